@@ -1,0 +1,241 @@
+#!/usr/bin/env python
+"""bench.py -- photons/s of the MI355X photon-mapping lightmap baker (BASELINE.json metric).
+
+A step = one full bake of the configuration's reference launch schedule (global_illumination_cl.c:
+215-272 flattened) over the synthetic scene resident in HBM: zero the int64 lightmap, trace every
+photon of this rank's shard, RCCL-reduce the per-GPU lightmaps to rank 0 (N > 1), finalise the float
+texels on rank 0. Host<->device copies of the geometry and texels are outside the timed region.
+
+  python bench.py [--gpus N --steps K --warmup W --config box200|box2000|example|box200-1e10]
+  N > 1: python -m torch.distributed.run --nproc-per-node N ... bench.py --gpus N
+
+Default (N=1): BASELINE config 3 -- synthetic 200-rectangle box, spa=172,413,793 = 1,000,012,800
+photons per step. Multi-GPU is weak scaling: spa x N photons per step, sharded evenly by work item.
+"""
+import argparse
+import ctypes
+import json
+import os
+import sys
+import time
+
+REPO = os.path.dirname(os.path.abspath(__file__))
+sys.path[:0] = [os.path.join(REPO, "flatmatch-global-illumination_amd"), os.path.join(REPO, "oracle")]
+
+import numpy as np  # noqa: E402
+
+CONFIGS = {
+    "box200": dict(scene="box200", spa=172_413_793, weak=True,
+                   desc="synthetic 200-rectangle box scene, 1e9 photons per GPU (BASELINE config 3)"),
+    "box200-1e10": dict(scene="box200", spa=1_724_137_931, weak=False,
+                        desc="synthetic 200-rectangle box scene, 1e10 photons sharded over N GPUs (BASELINE config 4)"),
+    "box2000": dict(scene="box2000", spa=172_413_793, weak=True,
+                    desc="synthetic 2000-rectangle box scene, 1e9 photons per GPU (BASELINE config 5)"),
+    "example": dict(scene="example", spa=6_500_000, weak=True,
+                    desc="example.png layout, 1e8 photons per GPU (BASELINE config 2)"),
+}
+METRIC = "photons/sec + achieved HBM GB/s (% of peak), 200-rect scene, 1/2/4/8 MI355X"
+FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector == FP32 matrix peak on gfx950
+HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+
+
+def load_scene(name):
+    from fmgi import scene
+
+    if name == "example":
+        return scene.load_geometry(os.path.join(REPO, "tests", "golden", "example_geometry.bin"), "example")
+    return scene.box_scene(int(name[3:]))
+
+
+def cpu_baseline(sc, spa, target_s=10.0):
+    """The oracle (plain-C restatement, OpenMP) timed on this host on a bounded prefix of the same
+    workload. Reported next to the GPU number, never used as the GPU result."""
+    import fm_oracle as O
+
+    threads = int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    offs = np.load(os.path.join(REPO, "tests", "golden", "glibc_rand_4096.npy"))
+    L = O.schedule_with_offsets(sc, spa, offs)
+    n = 64
+    while True:
+        t0 = time.perf_counter()
+        _, st = O.bake(sc, L, 0, n, nthreads=threads)
+        dt = time.perf_counter() - t0
+        if dt >= target_s or n >= 10_000_000:
+            break
+        n = int(n * min(8.0, max(1.5, 1.2 * target_s / max(dt, 1e-3))))
+    return {
+        "value": st["photons"] / dt,
+        "unit": "photons/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": f"oracle/fm_oracle.c on the first {n} work items ({st['photons']} photons) of the same "
+                  f"schedule, {dt:.1f} s, {threads} OpenMP threads",
+    }
+
+
+def pmc_traffic(config_name):
+    """HBM bytes per bake launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p))
+        return d.get(config_name, {}).get("hbm_bytes_per_launch")
+    except Exception:
+        return None
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=5)
+    ap.add_argument("--warmup", type=int, default=1)
+    ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
+    ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    args = ap.parse_args()
+
+    import torch
+    import torch.distributed as dist
+
+    import fmgi
+
+    rank = int(os.environ.get("RANK", "0"))
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    local = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
+    torch.cuda.set_device(local)
+    if world > 1:
+        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+
+    cfg = CONFIGS[args.config]
+    sc = load_scene(cfg["scene"])
+    spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
+    spa = min(spa, 2**31 - 1)
+    kernel = fmgi.KERNEL_FAST if args.kernel == "fast" else fmgi.KERNEL_EXACT
+
+    ctx = fmgi.Context(local)
+    ctx.set_scene(sc)
+    libc = ctypes.CDLL(None)
+    libc.srand(1)  # the unseeded state main.c runs with; every rank builds the same schedule
+    total_items = ctx.plan(spa)  # consumes rand() once per reference launch
+    b = total_items * rank // world
+    e = total_items * (rank + 1) // world
+    photons_per_step = 100 * total_items
+
+    dev = torch.device("cuda", local)
+    lm = torch.zeros((sc.num_texels, 4), dtype=torch.int64, device=dev)
+    tex_in = torch.zeros((sc.num_texels, 4), dtype=torch.float32, device=dev)
+    tex_out = torch.empty_like(tex_in)
+    stream = torch.cuda.current_stream()
+    sptr = stream.cuda_stream
+
+    k_ms = []
+
+    def step(timed):
+        lm.zero_()
+        if timed:
+            s_ev, e_ev = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+            s_ev.record(stream)
+        ctx.bake_items(b, e, lm.data_ptr(), kernel, sptr)
+        if timed:
+            e_ev.record(stream)
+            k_ms.append((s_ev, e_ev))
+        if world > 1:
+            dist.reduce(lm, dst=0)
+        if rank == 0:
+            ctx.finalize(lm.data_ptr(), tex_in.data_ptr(), tex_out.data_ptr(), sptr)
+
+    for _ in range(args.warmup):
+        step(False)
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        step(True)
+    torch.cuda.synchronize()
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    st = ctx.stats()
+    kernel_ms = float(np.mean([s.elapsed_time(x) for s, x in k_ms]))
+
+    vals = torch.tensor([elapsed, st["scans"], st["deposits"], st["photons"]], dtype=torch.float64, device=dev)
+    if world > 1:
+        t_max = vals[:1].clone()
+        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        sums = vals[1:].clone()
+        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        elapsed = float(t_max.item())
+        scans, deposits, photons_done = (float(x) for x in sums.tolist())
+    else:
+        scans, deposits, photons_done = float(st["scans"]), float(st["deposits"]), float(st["photons"])
+
+    if rank == 0:
+        assert int(photons_done) == photons_per_step * args.steps, (photons_done, photons_per_step)
+        value = photons_per_step * args.steps / elapsed
+        # rank 0's dominant kernel (the bake) per launch: SURVEY.md §8d algorithmic work
+        per_launch_scans = st["scans"] / args.steps
+        per_launch_deps = st["deposits"] / args.steps
+        flops = 40.0 * per_launch_scans * len(sc.walls) + 150.0 * per_launch_scans
+        hbm_bytes = 12.0 * per_launch_deps + 16.0 * sc.num_texels
+        ks = kernel_ms / 1e3
+        achieved_tf = flops / ks / 1e12
+        achieved_gbs = hbm_bytes / ks / 1e9
+        out = {
+            "metric": METRIC,
+            "value": value,
+            "unit": "photons/s",
+            "n_gpus": world,
+            "steps": args.steps,
+            "warmup": args.warmup,
+            "ms_per_step": elapsed / args.steps * 1e3,
+            "higher_is_better": True,
+            "scaling": "weak" if cfg["weak"] else "strong",
+            "vs_baseline": None,
+            "dtype": "f32",
+            "data": "synthetic (deterministic scene generator; seeds = unseeded glibc rand() as the reference)",
+            "config": {
+                "workload": cfg["desc"],
+                "scene": sc.name,
+                "rects": int(len(sc.walls)),
+                "texels": int(sc.num_texels),
+                "spa": spa,
+                "photons_per_step": photons_per_step,
+                "kernel": args.kernel,
+                "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
+            },
+            "roofline": {
+                "bound": "mfma",
+                "pipe": "fp32 VALU (no MFMA instructions; gfx950's dense FP32 peak is the same 157.3 TF for VALU and MFMA)",
+                "achieved": achieved_tf,
+                "peak": FP32_PEAK_TFLOPS,
+                "unit": "TFLOP/s",
+                "frac": achieved_tf / FP32_PEAK_TFLOPS,
+                "traffic": pmc_traffic(args.config),
+                "kernel_ms": kernel_ms,
+                "algorithmic_flops_per_launch": flops,
+                "hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                        "frac": achieved_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": hbm_bytes},
+            },
+            "per_photon": {
+                "scans": scans / photons_done,
+                "deposits": deposits / photons_done,
+                "rect_tests_evaluated": st["tests"] / max(st["photons"], 1),
+            },
+        }
+        if world == 1 and not args.no_cpu_baseline:
+            out["cpu_baseline"] = cpu_baseline(sc, cfg["spa"], args.cpu_seconds)
+        print(json.dumps(out), flush=True)
+    ctx.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,496 @@
+/*
+ * fmgi_api.cpp -- host side of libflatmatch_gi.so: the C ABI of include/flatmatch_gi.h.
+ *
+ * Replaces global_illumination_cl.c (the reference's OpenCL host driver):
+ *   - device selection / context / runtime compile (global_illumination_cl.c:102-212) become
+ *     hipGetDeviceCount/hipSetDevice and a code object linked into this library;
+ *   - photonMapLightSource's per-source sample count and launch loop (global_illumination_cl.c:215-272)
+ *     become fmgi_plan(): the same float arithmetic, the same `+1` work-group rounding, the same libc
+ *     rand() call per launch -- flattened into one work-item list that a single persistent kernel drains;
+ *   - performGlobalIlluminationCl (global_illumination_cl.c:275-321) keeps its signature and in-place
+ *     texel update; the texel buffer is accumulated exactly in int64 fixed point and added once.
+ * Compiled as host C++ with -ffp-contract=off: the per-rectangle precomputation below must produce the
+ * same IEEE fp32 bits photonmap.cl computes on the device.
+ */
+#include <hip/hip_runtime_api.h>
+
+#include <math.h>
+#include <stdarg.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+
+#include <algorithm>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/flatmatch_gi.h"
+#include "fmgi_internal.h"
+
+#define FMGI_API extern "C" __attribute__((visibility("default")))
+
+static_assert(sizeof(fmgi_rect) == 80, "Rectangle is 80 B (rectangle.h:19-26)");
+static_assert(sizeof(fmgi_geometry) == 80, "Geometry is 80 B (geometry.h:7-15)");
+static_assert(sizeof(fmgi_event) == 32, "fmgi_event is 32 B");
+static_assert(sizeof(fmgi_launch) == sizeof(LaunchDev), "launch layout");
+
+namespace {
+
+thread_local std::string g_err;
+
+int set_err(int code, const char *fmt, ...) {
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    g_err = buf;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                   \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) return set_err(FMGI_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_));    \
+    } while (0)
+
+f3 v3of(const fmgi_vec3 &v) { return mkf3(v.s[0], v.s[1], v.s[2]); }
+
+/* Host restatement of the per-rectangle values photonmap.cl recomputes per test (bit-identical). */
+RectDev make_rect(const fmgi_rect &r) {
+    RectDev d;
+    memset(&d, 0, sizeof d);
+    f3 pos = v3of(r.pos), w = v3of(r.width), h = v3of(r.height), n = v3of(r.n);
+    d.px = pos.x; d.py = pos.y; d.pz = pos.z;
+    d.nx = n.x; d.ny = n.y; d.nz = n.z;
+    float wl = len3(w), hl = len3(h);
+    f3 wn = div3(w, wl), hn = div3(h, hl);
+    d.wnx = wn.x; d.wny = wn.y; d.wnz = wn.z; d.wl = wl;
+    d.hnx = hn.x; d.hny = hn.y; d.hnz = hn.z; d.hl = hl;
+    d.base = r.lightmapSetup[0];
+    d.W = r.lightmapSetup[1];
+    d.H = r.lightmapSetup[2];
+    f3 bu, bv;
+    sampler_basis(n, bu, bv);
+    d.bux = bu.x; d.buy = bu.y; d.buz = bu.z;
+    d.bvx = bv.x; d.bvy = bv.y; d.bvz = bv.z;
+    d.axis = -1;
+    return d;
+}
+
+SrcDev make_src(const fmgi_rect &r) {
+    SrcDev s;
+    memset(&s, 0, sizeof s);
+    s.px = r.pos.s[0]; s.py = r.pos.s[1]; s.pz = r.pos.s[2];
+    s.wx = r.width.s[0]; s.wy = r.width.s[1]; s.wz = r.width.s[2];
+    s.hx = r.height.s[0]; s.hy = r.height.s[1]; s.hz = r.height.s[2];
+    s.nx = r.n.s[0]; s.ny = r.n.s[1]; s.nz = r.n.s[2];
+    f3 bu, bv;
+    sampler_basis(v3of(r.n), bu, bv);
+    s.bux = bu.x; s.buy = bu.y; s.buz = bu.z;
+    s.bvx = bv.x; s.bvy = bv.y; s.bvz = bv.z;
+    return s;
+}
+
+/* global_illumination_cl.c:217-222: area in float, (float)spa*area/100 -> uint64, then
+   (n / wg + 1) * wg (always at least one extra work group, as the reference does). */
+uint64_t source_items(const fmgi_rect &src, float spa, uint64_t wg) {
+    float area = len3(v3of(src.width)) * len3(v3of(src.height));
+    uint64_t n = (uint64_t)((spa * area) / 100);
+    return (n / wg + 1) * wg;
+}
+
+} // namespace
+
+struct fmgi_context {
+    int device = 0;
+    int num_cus = 256;
+    hipStream_t stream = nullptr;
+    RectDev *d_rects = nullptr;
+    int nrects = 0;
+    SrcDev *d_srcs = nullptr;
+    int nsrcs = 0, nwindows = 0, nlights = 0;
+    std::vector<fmgi_rect> h_srcs;
+    int num_texels = 0;
+    std::vector<LaunchDev> h_launches;
+    LaunchDev *d_launches = nullptr;
+    int64_t d_launch_cap = 0;
+    uint64_t total_items = 0;
+    unsigned long long *d_counter = nullptr;
+    unsigned long long *d_stats = nullptr;
+};
+
+FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
+FMGI_API const char *fmgi_last_error(void) { return g_err.c_str(); }
+
+FMGI_API int fmgi_device_count(void) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess) return 0;
+    return n;
+}
+
+FMGI_API void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n) {
+    for (int64_t i = 0; i < n; i++) fmgi_sincosf(x[i], &s[i], &c[i]);
+}
+
+FMGI_API fmgi_context *fmgi_create(int device) {
+    if (device == FMGI_HOST_ONLY) { /* schedule/scene logic only (CPU tests); bakes fail */
+        fmgi_context *c = new fmgi_context;
+        c->device = FMGI_HOST_ONLY;
+        return c;
+    }
+    int n = fmgi_device_count();
+    if (n <= 0) {
+        set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
+        return nullptr;
+    }
+    if (device < 0 || device >= n) {
+        set_err(FMGI_ERR_ARG, "device %d out of range (%d visible)", device, n);
+        return nullptr;
+    }
+    if (hipSetDevice(device) != hipSuccess) {
+        set_err(FMGI_ERR_HIP, "hipSetDevice(%d) failed", device);
+        return nullptr;
+    }
+    fmgi_context *c = new fmgi_context;
+    c->device = device;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, device) == hipSuccess && prop.multiProcessorCount > 0)
+        c->num_cus = prop.multiProcessorCount;
+    if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
+        hipMalloc(&c->d_counter, 64) != hipSuccess ||
+        hipMalloc(&c->d_stats, KSTAT_N * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_stats, 0, KSTAT_N * sizeof(unsigned long long)) != hipSuccess) {
+        set_err(FMGI_ERR_HIP, "context allocation failed on device %d", device);
+        fmgi_destroy(c);
+        return nullptr;
+    }
+    return c;
+}
+
+FMGI_API void fmgi_destroy(fmgi_context *c) {
+    if (!c) return;
+    if (c->device == FMGI_HOST_ONLY) {
+        delete c;
+        return;
+    }
+    hipSetDevice(c->device);
+    if (c->stream) hipStreamSynchronize(c->stream);
+    hipFree(c->d_rects);
+    hipFree(c->d_srcs);
+    hipFree(c->d_launches);
+    hipFree(c->d_counter);
+    hipFree(c->d_stats);
+    if (c->stream) hipStreamDestroy(c->stream);
+    delete c;
+}
+
+FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
+                            int num_windows, const fmgi_rect *lights, int num_lights, int num_texels) {
+    if (!c || num_walls < 0 || num_windows < 0 || num_lights < 0 || num_texels < 0 ||
+        (num_walls && !walls) || (num_windows && !windows) || (num_lights && !lights))
+        return set_err(FMGI_ERR_ARG, "fmgi_set_scene: bad arguments");
+    /* every texel index a deposit can produce must be inside the texel buffer */
+    for (int i = 0; i < num_walls; i++) {
+        const int32_t *lm = walls[i].lightmapSetup;
+        if (lm[1] < 1 || lm[2] < 1 || lm[0] < 0 || (int64_t)lm[0] + (int64_t)lm[1] * lm[2] > num_texels)
+            return set_err(FMGI_ERR_ARG, "wall %d: lightmapSetup {%d,%d,%d} outside %d texels", i, lm[0], lm[1],
+                           lm[2], num_texels);
+    }
+    std::vector<RectDev> rd((size_t)num_walls);
+    for (int i = 0; i < num_walls; i++) rd[i] = make_rect(walls[i]);
+    std::vector<SrcDev> sd;
+    c->h_srcs.clear();
+    for (int i = 0; i < num_windows; i++) { sd.push_back(make_src(windows[i])); c->h_srcs.push_back(windows[i]); }
+    for (int i = 0; i < num_lights; i++) { sd.push_back(make_src(lights[i])); c->h_srcs.push_back(lights[i]); }
+    if (c->device != FMGI_HOST_ONLY) {
+    HIPCHK(hipSetDevice(c->device));
+    hipFree(c->d_rects);
+    hipFree(c->d_srcs);
+    c->d_rects = nullptr;
+    c->d_srcs = nullptr;
+    if (num_walls) {
+        HIPCHK(hipMalloc(&c->d_rects, rd.size() * sizeof(RectDev)));
+        HIPCHK(hipMemcpy(c->d_rects, rd.data(), rd.size() * sizeof(RectDev), hipMemcpyHostToDevice));
+    }
+    if (!sd.empty()) {
+        HIPCHK(hipMalloc(&c->d_srcs, sd.size() * sizeof(SrcDev)));
+        HIPCHK(hipMemcpy(c->d_srcs, sd.data(), sd.size() * sizeof(SrcDev), hipMemcpyHostToDevice));
+    }
+    }
+    c->nrects = num_walls;
+    c->nsrcs = num_windows + num_lights;
+    c->nwindows = num_windows;
+    c->nlights = num_lights;
+    c->num_texels = num_texels;
+    c->h_launches.clear();
+    c->total_items = 0;
+    return FMGI_OK;
+}
+
+FMGI_API int64_t fmgi_plan_count(const fmgi_rect *windows, int num_windows, const fmgi_rect *lights, int num_lights,
+                                 int spa, int wg, uint64_t *total_items) {
+    if (wg <= 0) return set_err(FMGI_ERR_ARG, "wg must be > 0");
+    int64_t nl = 0;
+    uint64_t tot = 0, cap = (uint64_t)wg * 100;
+    for (int s = 0; s < num_windows + num_lights; s++) {
+        const fmgi_rect &r = s < num_windows ? windows[s] : lights[s - num_windows];
+        uint64_t n = source_items(r, (float)spa, (uint64_t)wg);
+        nl += (int64_t)((n + cap - 1) / cap);
+        tot += n;
+    }
+    if (total_items) *total_items = tot;
+    return nl;
+}
+
+FMGI_API int64_t fmgi_plan(fmgi_context *c, int spa, int wg, const int32_t *rng_offsets, int64_t n_offsets,
+                           uint64_t *total_items) {
+    if (!c || wg <= 0) return set_err(FMGI_ERR_ARG, "fmgi_plan: bad arguments");
+    std::vector<LaunchDev> L;
+    uint64_t item = 0, cap = (uint64_t)wg * 100;
+    int64_t k = 0;
+    for (int s = 0; s < c->nsrcs; s++) {
+        uint64_t n = source_items(c->h_srcs[s], (float)spa, (uint64_t)wg);
+        while (n) { /* global_illumination_cl.c:246-256 */
+            int32_t off;
+            if (rng_offsets) {
+                if (k >= n_offsets) return set_err(FMGI_ERR_ARG, "fmgi_plan: %lld rng offsets are not enough", (long long)n_offsets);
+                off = rng_offsets[k];
+            } else {
+                off = rand();
+            }
+            k++;
+            uint64_t ws = n < cap ? n : cap;
+            n -= ws;
+            LaunchDev d;
+            d.item_begin = item;
+            d.count = (uint32_t)ws;
+            d.rng_offset = off;
+            d.source = s;
+            d.is_window = s < c->nwindows;
+            L.push_back(d);
+            item += ws;
+        }
+    }
+    if (c->device != FMGI_HOST_ONLY) {
+    HIPCHK(hipSetDevice(c->device));
+    if ((int64_t)L.size() > c->d_launch_cap) {
+        hipFree(c->d_launches);
+        c->d_launches = nullptr;
+        c->d_launch_cap = 0;
+        HIPCHK(hipMalloc(&c->d_launches, L.size() * sizeof(LaunchDev)));
+        c->d_launch_cap = (int64_t)L.size();
+    }
+    if (!L.empty()) HIPCHK(hipMemcpy(c->d_launches, L.data(), L.size() * sizeof(LaunchDev), hipMemcpyHostToDevice));
+    }
+    c->h_launches.swap(L);
+    c->total_items = item;
+    if (total_items) *total_items = item;
+    return (int64_t)c->h_launches.size();
+}
+
+FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
+    if (!c) return set_err(FMGI_ERR_ARG, "null context");
+    int64_t n = (int64_t)c->h_launches.size();
+    if (out) memcpy(out, c->h_launches.data(), (size_t)std::min(n, cap) * sizeof(fmgi_launch));
+    return n;
+}
+
+static int grid_blocks(const fmgi_context *c, uint64_t items) {
+    /* persistent grid: 8 blocks of 256 lanes per CU (32 waves/CU); never more lanes than items */
+    uint64_t lanes_max = (uint64_t)c->num_cus * 8 * 256;
+    uint64_t lanes = std::min<uint64_t>(items, lanes_max);
+    return (int)std::max<uint64_t>(1, (lanes + 255) / 256);
+}
+
+static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
+                       void *events, int32_t *counts, uint32_t *rngf) {
+    if (!c || !lm) return set_err(FMGI_ERR_ARG, "fmgi_bake_items: bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context cannot bake");
+    if (e > c->total_items || b > e) return set_err(FMGI_ERR_ARG, "item range [%llu,%llu) outside plan of %llu items",
+                                                  (unsigned long long)b, (unsigned long long)e,
+                                                  (unsigned long long)c->total_items);
+    if (b == e) return FMGI_OK;
+    if (c->nrects == 0 || c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
+    HIPCHK(hipSetDevice(c->device));
+    BakeArgs a;
+    memset(&a, 0, sizeof a);
+    a.rects = c->d_rects;
+    a.nrects = c->nrects;
+    a.srcs = c->d_srcs;
+    a.launches = c->d_launches;
+    a.nlaunches = (int)c->h_launches.size();
+    a.item_begin = b;
+    a.item_end = e;
+    a.counter = c->d_counter;
+    a.lm = (unsigned long long *)lm;
+    a.stats = c->d_stats;
+    a.events = events;
+    a.ev_counts = counts;
+    a.rng_final = rngf;
+    HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
+    HIPCHK(fmgi_launch_bake(a, kernel, trace, grid_blocks(c, e - b), s));
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_bake_items(fmgi_context *c, uint64_t item_begin, uint64_t item_end, void *lm_fx_dev, int kernel,
+                             void *stream) {
+    if (!c) return set_err(FMGI_ERR_ARG, "null context");
+    return bake_common(c, item_begin, item_end, lm_fx_dev, kernel, stream ? (hipStream_t)stream : c->stream, false,
+                       nullptr, nullptr, nullptr);
+}
+
+FMGI_API int fmgi_finalize(fmgi_context *c, const void *lm, const void *tin, void *tout, void *stream) {
+    if (!c || !lm || !tin || !tout) return set_err(FMGI_ERR_ARG, "fmgi_finalize: bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(fmgi_launch_finalize((const unsigned long long *)lm, (const float *)tin, (float *)tout, c->num_texels,
+                                stream ? (hipStream_t)stream : c->stream));
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_get_stats(fmgi_context *c, fmgi_stats *out) {
+    if (!c || !out) return set_err(FMGI_ERR_ARG, "bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long v[KSTAT_N];
+    HIPCHK(hipMemcpy(v, c->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    memset(out, 0, sizeof *out);
+    out->photons = v[KSTAT_PHOTONS];
+    out->scans = v[KSTAT_SCANS];
+    out->deposits = v[KSTAT_DEPOSITS];
+    out->escapes = v[KSTAT_ESCAPES];
+    out->exact_rescans = v[KSTAT_RESCANS];
+    out->tests = v[KSTAT_TESTS];
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_reset_stats(fmgi_context *c) {
+    if (!c) return set_err(FMGI_ERR_ARG, "null context");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemset(c->d_stats, 0, KSTAT_N * sizeof(unsigned long long)));
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_trace_items(fmgi_context *c, uint64_t b, uint64_t e, int kernel, fmgi_event *events,
+                              int32_t *counts, uint32_t *rng_final) {
+    if (!c || !events || !counts || !rng_final || e < b || e - b > 4096)
+        return set_err(FMGI_ERR_ARG, "fmgi_trace_items: bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    uint64_t n = e - b;
+    if (!n) return FMGI_OK;
+    HIPCHK(hipSetDevice(c->device));
+    void *d_ev = nullptr, *d_cnt = nullptr, *d_rng = nullptr, *d_lm = nullptr;
+    size_t ev_bytes = (size_t)n * FMGI_EVENTS_PER_ITEM * sizeof(fmgi_event);
+    size_t lm_bytes = (size_t)c->num_texels * 4 * sizeof(unsigned long long);
+    int rc = FMGI_OK;
+    if (hipMalloc(&d_ev, ev_bytes) != hipSuccess || hipMalloc(&d_cnt, n * 4) != hipSuccess ||
+        hipMalloc(&d_rng, n * 4) != hipSuccess || hipMalloc(&d_lm, lm_bytes ? lm_bytes : 32) != hipSuccess) {
+        rc = set_err(FMGI_ERR_OOM, "trace buffers");
+    } else {
+        hipMemset(d_lm, 0, lm_bytes ? lm_bytes : 32);
+        hipMemset(d_cnt, 0, n * 4);
+        rc = bake_common(c, b, e, d_lm, kernel, c->stream, true, d_ev, (int32_t *)d_cnt, (uint32_t *)d_rng);
+        if (rc == FMGI_OK) {
+            hipError_t err = hipStreamSynchronize(c->stream);
+            if (err == hipSuccess) err = hipMemcpy(events, d_ev, ev_bytes, hipMemcpyDeviceToHost);
+            if (err == hipSuccess) err = hipMemcpy(counts, d_cnt, n * 4, hipMemcpyDeviceToHost);
+            if (err == hipSuccess) err = hipMemcpy(rng_final, d_rng, n * 4, hipMemcpyDeviceToHost);
+            if (err != hipSuccess) rc = set_err(FMGI_ERR_HIP, "trace: %s", hipGetErrorString(err));
+        }
+    }
+    hipFree(d_ev);
+    hipFree(d_cnt);
+    hipFree(d_rng);
+    hipFree(d_lm);
+    return rc;
+}
+
+FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, float *co, int64_t n) {
+    if (!c || n < 0) return set_err(FMGI_ERR_ARG, "bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    if (!n) return FMGI_OK;
+    HIPCHK(hipSetDevice(c->device));
+    float *d = nullptr;
+    HIPCHK(hipMalloc(&d, (size_t)n * 12));
+    hipError_t err = hipMemcpy(d, x, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = fmgi_launch_sincos(d, d + n, d + 2 * n, n, c->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+    if (err == hipSuccess) err = hipMemcpy(s, d + n, (size_t)n * 4, hipMemcpyDeviceToHost);
+    if (err == hipSuccess) err = hipMemcpy(co, d + 2 * n, (size_t)n * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (err != hipSuccess) return set_err(FMGI_ERR_HIP, "device sincos: %s", hipGetErrorString(err));
+    return FMGI_OK;
+}
+
+/* ---- the drop-in entry points ----------------------------------------------------------------- */
+
+static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_out, bool verbose) {
+    if (!geo) return set_err(FMGI_ERR_ARG, "null geometry");
+    const char *wg_env = getenv("FMGI_WG");
+    int wg = wg_env ? atoi(wg_env) : 256;
+    if (wg <= 0) wg = 256;
+    const char *k_env = getenv("FMGI_KERNEL");
+    int kernel = (k_env && !strcmp(k_env, "exact")) ? FMGI_KERNEL_EXACT : FMGI_KERNEL_FAST;
+    int ndev = fmgi_device_count();
+    if (ndev <= 0) return set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
+    fmgi_context *c = fmgi_create(0);
+    if (!c) return FMGI_ERR_HIP;
+    int rc = fmgi_set_scene(c, geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
+                            geo->numLights, geo->numTexels);
+    uint64_t items = 0;
+    if (rc == FMGI_OK) {
+        int64_t nl = fmgi_plan(c, spa, wg, nullptr, 0, &items);
+        if (nl < 0) rc = (int)nl;
+        else if (verbose) {
+            hipDeviceProp_t prop;
+            hipGetDeviceProperties(&prop, c->device);
+            printf("[INF] Selected device '%s'\n\n", prop.name);
+            printf("photon-mapping %d light sources with %llu M samples in %lld reference launches\n",
+                   c->nsrcs, (unsigned long long)(items * 100 / 1000000), (long long)nl);
+            fflush(stdout);
+        }
+    }
+    size_t tb = (size_t)geo->numTexels * 16;
+    void *d_lm = nullptr, *d_tex = nullptr;
+    if (rc == FMGI_OK && geo->numTexels > 0) {
+        if (hipMalloc(&d_lm, tb * 2) != hipSuccess || hipMalloc(&d_tex, tb) != hipSuccess) {
+            rc = set_err(FMGI_ERR_OOM, "texel buffers (%zu B)", tb * 3);
+        } else if (hipMemsetAsync(d_lm, 0, tb * 2, c->stream) != hipSuccess ||
+                   hipMemcpyAsync(d_tex, geo->texels, tb, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
+            rc = set_err(FMGI_ERR_HIP, "texel upload");
+        }
+        if (rc == FMGI_OK) rc = fmgi_bake_items(c, 0, items, d_lm, kernel, c->stream);
+        if (rc == FMGI_OK) rc = fmgi_finalize(c, d_lm, d_tex, d_tex, c->stream);
+        if (rc == FMGI_OK) {
+            hipError_t e = hipMemcpyAsync(texels_out, d_tex, tb, hipMemcpyDeviceToHost, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            if (e != hipSuccess) rc = set_err(FMGI_ERR_HIP, "bake: %s", hipGetErrorString(e));
+        }
+    }
+    hipFree(d_lm);
+    hipFree(d_tex);
+    fmgi_destroy(c);
+    return rc;
+}
+
+FMGI_API int getGlobalIlluminationCl(const fmgi_geometry *geo, int numSamplesPerArea, fmgi_vec3 *texels_out) {
+    if (!geo || (geo->numTexels > 0 && (!texels_out || !geo->texels)))
+        return set_err(FMGI_ERR_ARG, "getGlobalIlluminationCl: bad arguments");
+    return bake_geometry(geo, numSamplesPerArea, texels_out, false);
+}
+
+FMGI_API void performGlobalIlluminationCl(fmgi_geometry *geo, int numSamplesPerArea) {
+    const char *q = getenv("FMGI_QUIET");
+    int rc = bake_geometry(geo, numSamplesPerArea, geo ? geo->texels : nullptr, !(q && atoi(q)));
+    if (rc != FMGI_OK) {
+        /* the reference's fatal-error convention: message on stdout, exit(-1) (global_illumination_cl.c:263) */
+        printf("[Err] performGlobalIlluminationCl: %s\n", fmgi_last_error());
+        fflush(stdout);
+        exit(-1);
+    }
+}

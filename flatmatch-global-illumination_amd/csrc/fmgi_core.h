@@ -1,0 +1,150 @@
+/*
+ * fmgi_core.h -- device-side data layout and the exact photon-step arithmetic.
+ *
+ * Everything in this header is evaluated with IEEE fp32 ops in the order of photonmap.cl
+ * (this translation unit is compiled with -ffp-contract=off and correctly rounded div/sqrt), so the
+ * results are bit-identical to the oracle contract (oracle/fm_oracle.h). It is shared by the exact
+ * kernel, the fast kernel's verification step and the host-side precomputation.
+ */
+#ifndef FMGI_CORE_H
+#define FMGI_CORE_H
+
+#include <stdint.h>
+#include <math.h>
+
+#include "fmgi_math.h"
+
+#if defined(__clang__)
+#pragma clang fp contract(off)
+#endif
+
+#define FMGI_FX_SHIFT 25        /* fixed point: one unit = 2^-25 (every deposit channel is a multiple) */
+#define FMGI_PHOTONS_PER_ITEM 100 /* photonmap.cl:279 */
+#define FMGI_MAX_DEPTH 8          /* photonmap.cl:171 */
+#define FMGI_EVENTS_PER_ITEM (FMGI_PHOTONS_PER_ITEM * FMGI_MAX_DEPTH)
+
+struct f3 { float x, y, z; };
+
+FMGI_HD f3 mkf3(float x, float y, float z) { f3 r; r.x = x; r.y = y; r.z = z; return r; }
+FMGI_HD f3 add3(f3 a, f3 b) { return mkf3(a.x + b.x, a.y + b.y, a.z + b.z); }
+FMGI_HD f3 sub3(f3 a, f3 b) { return mkf3(a.x - b.x, a.y - b.y, a.z - b.z); }
+FMGI_HD f3 mul3(f3 a, float s) { return mkf3(a.x * s, a.y * s, a.z * s); }
+FMGI_HD f3 div3(f3 a, float s) { return mkf3(a.x / s, a.y / s, a.z / s); }
+/* OpenCL dot/cross/length/normalize as fixed by the parity contract */
+FMGI_HD float dot3(f3 a, f3 b) { float t = a.x * b.x; t = t + a.y * b.y; return t + a.z * b.z; }
+FMGI_HD f3 cross3(f3 a, f3 b) { return mkf3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
+FMGI_HD float len3(f3 a) { return sqrtf(dot3(a, a)); }
+FMGI_HD f3 normalize3(f3 a) { return div3(a, len3(a)); }
+
+/*
+ * One wall rectangle as the kernels read it: 128 B (two s_load_dwordx16). Exact fields are the
+ * reference Rectangle plus values photonmap.cl recomputes per test, hoisted to the host with the same
+ * IEEE ops (bit-identical): wn = width/length(width) (photonmap.cl:145), wl = length(width) (:144),
+ * hn/hl likewise (:149-150), and the sampler basis of the normal (bu, bv; photonmap.cl:65-70).
+ * The last 8 words are the fast kernel's conservative filter constants (see fmgi_kernels.hip).
+ */
+struct __attribute__((aligned(16))) RectDev {
+    float px, py, pz;      /* pos                      */
+    float nx, ny, nz;      /* n                        */
+    float wnx, wny, wnz;   /* width / length(width)     */
+    float wl;              /* length(width)            */
+    float hnx, hny, hnz;   /* height / length(height)   */
+    float hl;              /* length(height)           */
+    int32_t base, W, H;    /* lightmapSetup.s0/s1/s2    */
+    int32_t axis;          /* filter class: 0..5 = axis-aligned normal (+x,-x,+y,-y,+z,-z), -1 general */
+    float bux, buy, buz;   /* sampler basis udir        */
+    float bvx, bvy, bvz;   /* sampler basis vdir        */
+    float f[8];            /* filter constants          */
+};
+static_assert(sizeof(RectDev) == 128, "RectDev must be 128 B");
+
+/* One emitter (window or light), photonmap.cl:173-181. */
+struct __attribute__((aligned(16))) SrcDev {
+    float px, py, pz, wx, wy, wz, hx, hy, hz, nx, ny, nz;
+    float bux, buy, buz, bvx, bvy, bvz;
+    float pad[14];
+};
+static_assert(sizeof(SrcDev) == 128, "SrcDev must be 128 B");
+
+struct LaunchDev {
+    uint64_t item_begin;
+    uint32_t count;
+    int32_t rng_offset;
+    int32_t source;
+    int32_t is_window;
+};
+static_assert(sizeof(LaunchDev) == 24, "LaunchDev must be 24 B");
+
+/* photonmap.cl:21-25 */
+FMGI_HD float rng_next(uint32_t &s) {
+    s = s * 1664525u + 1013904223u;
+    return (float)s * 2.3283064365386963e-10f; /* == (float)s / (float)0xFFFFFFFF, an exact 2^-32 scale */
+}
+
+/* Sampler basis for a normal: photonmap.cl:43-48 (== :65-70). Host-side precomputation. */
+FMGI_HD void sampler_basis(f3 n, f3 &bu, f3 &bv) {
+    f3 udir = mkf3(0, 0, 1);
+    if (fabsf(dot3(udir, n)) >= 0.999999f) udir = mkf3(0, 1, 0);
+    f3 vdir = normalize3(cross3(udir, n));
+    udir = normalize3(cross3(vdir, n));
+    bu = udir;
+    bv = vdir;
+}
+
+/* photonmap.cl:27-74 with the basis precomputed: fold=1 is the window ("sky") sampler. */
+FMGI_HD f3 sample_dir(uint32_t &rng, f3 n, f3 bu, f3 bv, bool fold) {
+    float r = sqrtf(rng_next(rng));
+    float phi = 6.283184f * rng_next(rng);
+    float sn, cs;
+    fmgi_sincosf(phi, &sn, &cs);
+    float u = r * cs;
+    float v = r * sn;
+    float w = sqrtf(1.0f - r * r);
+    if (fold && u < 0) u = -u;
+    return add3(add3(mul3(bu, u), mul3(bv, v)), mul3(n, w));
+}
+
+/* photonmap.cl:123-158; wn/wl/hn/hl are the hoisted, bit-identical per-rect values. */
+FMGI_HD float intersect_exact(f3 n, f3 pos, f3 wn, float wl, f3 hn, float hl, f3 src, f3 dir, float closest) {
+    float denom = dot3(n, dir);
+    if (denom >= 0) return -1;
+    float fac = dot3(n, sub3(pos, src)) / denom;
+    if (fac < 0) return -1;
+    f3 ray = mul3(dir, fac);
+    if (closest * closest < dot3(ray, ray)) return -1;
+    f3 pDir = sub3(add3(src, ray), pos);
+    float dx = dot3(wn, pDir);
+    if (dx < 0 || dx > wl) return -1;
+    float dy = dot3(hn, pDir);
+    if (dy < 0 || dy > hl) return -1;
+    return fac;
+}
+
+/* photonmap.cl:95-120 */
+FMGI_HD int tile_at(f3 pos, f3 wn, float wl, f3 hn, float hl, int W, int H, f3 p) {
+    f3 pDir = sub3(p, pos);
+    float dx = dot3(wn, pDir);
+    float dy = dot3(hn, pDir);
+    int tx = (int)(dx * (float)W / wl);
+    int ty = (int)(dy * (float)H / hl);
+    tx = tx < 0 ? 0 : (tx > W - 1 ? W - 1 : tx);
+    ty = ty < 0 ? 0 : (ty > H - 1 ? H - 1 : ty);
+    return ty * W + tx;
+}
+
+/* Warm-up skip-ahead (photonmap.cl:272-275): `r = rand()*40; for (i=0; i<r; i++) rand();` draws
+   ceil(r) values; LCG^k(s) = A[k]*s + C[k]. */
+struct LcgJump { uint32_t a[41], c[41]; };
+
+inline void lcg_jump_table(LcgJump &t) {
+    uint32_t a = 1, c = 0;
+    for (int k = 0; k <= 40; k++) {
+        t.a[k] = a;
+        t.c[k] = c;
+        /* compose one more step: s' = 1664525*(a*s + c) + 1013904223 */
+        a = 1664525u * a;
+        c = 1664525u * c + 1013904223u;
+    }
+}
+
+#endif

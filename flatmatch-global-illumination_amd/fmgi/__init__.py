@@ -1,0 +1,186 @@
+"""fmgi -- Python mirror of the MI355X photon-mapping lightmap baker's C ABI.
+
+The product is libflatmatch_gi.so (HIP kernels for gfx950 + the C ABI of include/flatmatch_gi.h);
+this package only binds it with ctypes for tests, bench.py and Python callers:
+
+  * ``Context``      -- fmgi_create / fmgi_set_scene / fmgi_plan / fmgi_bake_items / fmgi_finalize;
+  * ``bake_geometry`` -- getGlobalIlluminationCl on host arrays (the reference's
+                         performGlobalIlluminationCl semantics, global_illumination_cl.c:275-321);
+  * ``scene``        -- the Rectangle/Geometry layout, fixtures and synthetic box scenes.
+
+Device buffers are passed as plain integer addresses (e.g. ``torch.Tensor.data_ptr()``) and streams as
+``hipStream_t`` integers; no torch type crosses the C ABI.
+"""
+from __future__ import annotations
+
+import ctypes as C
+
+import numpy as np
+
+from . import scene
+from ._lib import KERNEL_EXACT, KERNEL_FAST, FmgiError, Geometry, Stats, check, load
+from .scene import RECT_DTYPE, Scene
+
+LAUNCH_DTYPE = np.dtype(
+    [("item_begin", "<u8"), ("count", "<u4"), ("rng_offset", "<i4"), ("source", "<i4"), ("is_window", "<i4")]
+)
+assert LAUNCH_DTYPE.itemsize == 24
+EVENT_DTYPE = np.dtype(
+    [("photon", "<i4"), ("depth", "<i4"), ("rect", "<i4"), ("texel", "<i4"), ("rgb", "<f4", 3), ("rng", "<u4")]
+)
+assert EVENT_DTYPE.itemsize == 32
+EVENTS_PER_ITEM = 800
+FX_SHIFT = 25
+
+__all__ = [
+    "Context",
+    "bake_geometry",
+    "plan_count",
+    "scene",
+    "Scene",
+    "FmgiError",
+    "KERNEL_EXACT",
+    "KERNEL_FAST",
+    "LAUNCH_DTYPE",
+    "EVENT_DTYPE",
+    "device_count",
+    "host_sincosf",
+]
+
+
+def _ptr(a: np.ndarray | None):
+    if a is None or len(a) == 0:
+        return None
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data_as(C.c_void_p)
+
+
+def device_count() -> int:
+    return int(load().fmgi_device_count())
+
+
+def host_sincosf(x):
+    """Host fmgi_sincosf over an array (bit-identical to the device sampler's sin/cos)."""
+    x = np.ascontiguousarray(np.atleast_1d(x), np.float32)
+    s = np.empty_like(x)
+    c = np.empty_like(x)
+    load().fmgi_host_sincosf(_ptr(x), _ptr(s), _ptr(c), len(x))
+    return s, c
+
+
+def plan_count(sc: Scene, spa: int, wg: int = 256):
+    """(launches, work items) of the reference schedule, without consuming rand()."""
+    tot = C.c_uint64()
+    w = np.ascontiguousarray(sc.windows)
+    l = np.ascontiguousarray(sc.lights)
+    n = check(load().fmgi_plan_count(_ptr(w), len(w), _ptr(l), len(l), spa, wg, C.byref(tot)), "fmgi_plan_count")
+    return int(n), int(tot.value)
+
+
+class Context:
+    """One device's baker state (fmgi_context)."""
+
+    def __init__(self, device: int = 0):
+        self.lib = load()
+        self.h = self.lib.fmgi_create(device)
+        if not self.h:
+            raise FmgiError(f"fmgi_create({device}): {self.lib.fmgi_last_error().decode()}")
+        self.device = device
+        self.scene: Scene | None = None
+        self.total_items = 0
+        self.nlaunches = 0
+
+    def close(self):
+        if self.h:
+            self.lib.fmgi_destroy(self.h)
+            self.h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    def set_scene(self, sc: Scene):
+        self._keep = [np.ascontiguousarray(a) for a in (sc.walls, sc.windows, sc.lights)]
+        w, win, li = self._keep
+        check(
+            self.lib.fmgi_set_scene(self.h, _ptr(w), len(w), _ptr(win), len(win), _ptr(li), len(li), sc.num_texels),
+            "fmgi_set_scene",
+        )
+        self.scene = sc
+
+    def plan(self, spa: int, wg: int = 256, rng_offsets=None) -> int:
+        """Reference launch schedule. rng_offsets=None consumes libc rand() like the reference."""
+        tot = C.c_uint64()
+        offs = None if rng_offsets is None else np.ascontiguousarray(rng_offsets, np.int32)
+        n = check(
+            self.lib.fmgi_plan(self.h, spa, wg, _ptr(offs), 0 if offs is None else len(offs), C.byref(tot)),
+            "fmgi_plan",
+        )
+        self.total_items = int(tot.value)
+        self.nlaunches = int(n)
+        return self.total_items
+
+    def get_plan(self) -> np.ndarray:
+        out = np.zeros(self.nlaunches, LAUNCH_DTYPE)
+        check(self.lib.fmgi_get_plan(self.h, _ptr(out), len(out)), "fmgi_get_plan")
+        return out
+
+    def bake_items(self, begin: int, end: int, lm_fx_ptr: int, kernel: int = KERNEL_FAST, stream: int = 0):
+        check(self.lib.fmgi_bake_items(self.h, begin, end, C.c_void_p(lm_fx_ptr), kernel, C.c_void_p(stream or None)),
+              "fmgi_bake_items")
+
+    def finalize(self, lm_fx_ptr: int, texels_in_ptr: int, texels_out_ptr: int, stream: int = 0):
+        check(
+            self.lib.fmgi_finalize(self.h, C.c_void_p(lm_fx_ptr), C.c_void_p(texels_in_ptr), C.c_void_p(texels_out_ptr),
+                                   C.c_void_p(stream or None)),
+            "fmgi_finalize",
+        )
+
+    def stats(self) -> dict:
+        st = Stats()
+        check(self.lib.fmgi_get_stats(self.h, C.byref(st)), "fmgi_get_stats")
+        return st.as_dict()
+
+    def reset_stats(self):
+        check(self.lib.fmgi_reset_stats(self.h), "fmgi_reset_stats")
+
+    def trace_items(self, begin: int, end: int, kernel: int = KERNEL_FAST):
+        """Per-photon bounce records of items [begin, end): (events[n, 800], counts[n], rng_final[n])."""
+        n = end - begin
+        ev = np.zeros(n * EVENTS_PER_ITEM, EVENT_DTYPE)
+        cnt = np.zeros(n, np.int32)
+        rng = np.zeros(n, np.uint32)
+        check(self.lib.fmgi_trace_items(self.h, begin, end, kernel, _ptr(ev), _ptr(cnt), _ptr(rng)), "fmgi_trace_items")
+        return ev.reshape(n, EVENTS_PER_ITEM), cnt, rng
+
+    def device_sincosf(self, x: np.ndarray):
+        x = np.ascontiguousarray(x, np.float32)
+        s = np.empty_like(x)
+        c = np.empty_like(x)
+        check(self.lib.fmgi_device_sincosf(self.h, _ptr(x), _ptr(s), _ptr(c), len(x)), "fmgi_device_sincosf")
+        return s, c
+
+
+def make_geometry(sc: Scene, texels: np.ndarray):
+    """A reference Geometry struct pointing at numpy arrays (kept alive by the returned tuple)."""
+    keep = [np.ascontiguousarray(a) for a in (sc.windows, sc.lights, sc.walls)]
+    g = Geometry()
+    g.windows, g.lights, g.walls = (a.ctypes.data if len(a) else None for a in keep)
+    g.boxWalls = None
+    g.numWindows, g.numLights, g.numWalls = len(keep[0]), len(keep[1]), len(keep[2])
+    g.numBoxWalls = 0
+    g.numTexels = sc.num_texels
+    g.texels = texels.ctypes.data
+    return g, keep
+
+
+def bake_geometry(sc: Scene, spa: int, texels: np.ndarray | None = None) -> np.ndarray:
+    """getGlobalIlluminationCl: bake on host arrays; consumes libc rand() like the reference."""
+    tin = sc.texels() if texels is None else np.ascontiguousarray(texels, np.float32)
+    out = np.empty_like(tin)
+    g, keep = make_geometry(sc, tin)
+    check(load().getGlobalIlluminationCl(C.byref(g), spa, out.ctypes.data_as(C.c_void_p)), "getGlobalIlluminationCl")
+    del keep
+    return out

@@ -1,0 +1,129 @@
+"""ctypes binding of libflatmatch_gi.so (include/flatmatch_gi.h). No fallback: if the HIP library is
+missing or a call fails, an exception is raised -- there is no CPU path in the product."""
+from __future__ import annotations
+
+import ctypes as C
+import os
+
+PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+LIB_PATH = os.path.join(PKG_DIR, "libflatmatch_gi.so")
+
+# Exported symbols of the C ABI (tests check the built library exports exactly these + nothing
+# that would clash with the reference objects main.c links against).
+EXPORTS = (
+    "performGlobalIlluminationCl",
+    "getGlobalIlluminationCl",
+    "fmgi_version",
+    "fmgi_last_error",
+    "fmgi_device_count",
+    "fmgi_create",
+    "fmgi_destroy",
+    "fmgi_set_scene",
+    "fmgi_plan",
+    "fmgi_get_plan",
+    "fmgi_plan_count",
+    "fmgi_bake_items",
+    "fmgi_finalize",
+    "fmgi_get_stats",
+    "fmgi_reset_stats",
+    "fmgi_trace_items",
+    "fmgi_host_sincosf",
+    "fmgi_device_sincosf",
+)
+
+KERNEL_EXACT = 0
+KERNEL_FAST = 1
+
+
+class FmgiError(RuntimeError):
+    pass
+
+
+class Stats(C.Structure):
+    _fields_ = [
+        ("photons", C.c_uint64),
+        ("scans", C.c_uint64),
+        ("deposits", C.c_uint64),
+        ("escapes", C.c_uint64),
+        ("exact_rescans", C.c_uint64),
+        ("tests", C.c_uint64),
+        ("reserved", C.c_uint64 * 2),
+    ]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "reserved"}
+
+
+class Geometry(C.Structure):
+    """geometry.h:7-15 (80 B)."""
+
+    _fields_ = [
+        ("windows", C.c_void_p),
+        ("lights", C.c_void_p),
+        ("walls", C.c_void_p),
+        ("boxWalls", C.c_void_p),
+        ("numWindows", C.c_int32),
+        ("numLights", C.c_int32),
+        ("numWalls", C.c_int32),
+        ("numBoxWalls", C.c_int32),
+        ("width", C.c_int32),
+        ("height", C.c_int32),
+        ("startingPositionX", C.c_float),
+        ("startingPositionY", C.c_float),
+        ("numTexels", C.c_int32),
+        ("texels", C.c_void_p),
+    ]
+
+
+assert C.sizeof(Geometry) == 80
+
+_lib = None
+
+
+def load() -> C.CDLL:
+    """Load the in-tree HIP library (built by __graft_entry__.build() / `make -C <pkg>`)."""
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise FmgiError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` (no CPU fallback exists)")
+    lib = C.CDLL(LIB_PATH)
+    vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
+    sig = {
+        "fmgi_version": (C.c_char_p, []),
+        "fmgi_last_error": (C.c_char_p, []),
+        "fmgi_device_count": (C.c_int, []),
+        "fmgi_create": (vp, [C.c_int]),
+        "fmgi_destroy": (None, [vp]),
+        "fmgi_set_scene": (C.c_int, [vp, vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int]),
+        "fmgi_plan": (i64, [vp, C.c_int, C.c_int, vp, i64, C.POINTER(u64)]),
+        "fmgi_get_plan": (i64, [vp, vp, i64]),
+        "fmgi_plan_count": (i64, [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.POINTER(u64)]),
+        "fmgi_bake_items": (C.c_int, [vp, u64, u64, vp, C.c_int, vp]),
+        "fmgi_finalize": (C.c_int, [vp, vp, vp, vp, vp]),
+        "fmgi_get_stats": (C.c_int, [vp, C.POINTER(Stats)]),
+        "fmgi_reset_stats": (C.c_int, [vp]),
+        "fmgi_trace_items": (C.c_int, [vp, u64, u64, C.c_int, vp, vp, vp]),
+        "fmgi_host_sincosf": (None, [vp, vp, vp, i64]),
+        "fmgi_device_sincosf": (C.c_int, [vp, vp, vp, vp, i64]),
+        "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
+        "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),
+    }
+    for name, (res, args) in sig.items():
+        f = getattr(lib, name)
+        f.restype = res
+        f.argtypes = args
+    _ = i32
+    _lib = lib
+    return lib
+
+
+def last_error() -> str:
+    msg = load().fmgi_last_error()
+    return msg.decode() if msg else ""
+
+
+def check(rc: int, what: str) -> int:
+    if rc < 0:
+        raise FmgiError(f"{what} failed ({rc}): {last_error()}")
+    return rc

@@ -1,0 +1,161 @@
+/*
+ * flatmatch_gi.h -- C ABI of libflatmatch_gi.so, the MI355X-native drop-in for the reference's
+ * OpenCL photon-mapping path (rbuch703/flatmatch-global-illumination).
+ *
+ * Drop-in entry point (replaces global_illumination_cl.c:275-321, declared at
+ * global_illumination_cl.h:10):
+ *
+ *     void performGlobalIlluminationCl(Geometry *geo, int numSamplesPerArea);
+ *
+ * The reference's main.c (main.c:63) links against this library unchanged: it includes its own
+ * global_illumination_cl.h; the symbol name, argument meaning, in-place texel update and fatal-error
+ * behaviour (message on stdout + exit(-1), global_illumination_cl.c:254,263) are the reference's.
+ * libc rand() is consumed once per kernel launch of the reference schedule
+ * (global_illumination_cl.c:251), so RNG seeds and post-call libc state match the reference.
+ *
+ * Everything else here is build-defined (prefix fmgi_) and exists so tests and bench.py can drive
+ * the device-resident path with plain pointers: no torch or HIP types cross this boundary
+ * (streams are passed as void* hipStream_t, device buffers as void*).
+ *
+ * Environment knobs the reference ABI cannot carry (read by performGlobalIlluminationCl):
+ *   FMGI_WG        virtual OpenCL work-group size of the launch schedule (default 256, the value
+ *                  ROCm's OpenCL reports for CL_KERNEL_WORK_GROUP_SIZE; global_illumination_cl.c:300)
+ *   FMGI_GPUS      number of GPUs to shard over (default: all visible, max 8)
+ *   FMGI_KERNEL    "fast" (default) or "exact" -- both produce identical bits; see DESIGN.md
+ *   FMGI_QUIET     1 = suppress the reference's progress line
+ */
+#ifndef FLATMATCH_GI_H
+#define FLATMATCH_GI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ---- Layout-identical equivalents of the reference ABI types (no CL headers needed). ---------- */
+/* Vector3 == cl_float4 (vector3_cl.h:14): 16 B, 16-B aligned; .s[3] unused.                      */
+typedef struct __attribute__((aligned(16))) fmgi_vec3 { float s[4]; } fmgi_vec3;
+/* Rectangle (rectangle.h:19-26): 80 B, 16-B aligned. lightmapSetup = {texel base, tiles along
+   width, tiles along height, 0}. Windows/lights have lightmapSetup.s0 == 0.                       */
+typedef struct __attribute__((aligned(16))) fmgi_rect {
+    fmgi_vec3 pos, width, height, n;
+    int32_t lightmapSetup[4];
+} fmgi_rect;
+/* Geometry (geometry.h:7-15): 80 B. boxWalls are not used by the photon-mapping path.             */
+typedef struct fmgi_geometry {
+    fmgi_rect *windows, *lights, *walls, *boxWalls;
+    int32_t numWindows, numLights, numWalls, numBoxWalls;
+    int32_t width, height;
+    float startingPositionX, startingPositionY;
+    int32_t numTexels;
+    fmgi_vec3 *texels;
+} fmgi_geometry;
+
+/* ---- Drop-in entry points ----------------------------------------------------------------------- */
+#ifndef GLOBAL_ILLUMINATION_CL /* the reference header declares it with its own Geometry type */
+void performGlobalIlluminationCl(fmgi_geometry *geo, int numSamplesPerArea);
+#endif
+/* North-star name, build-defined (the reference has no such symbol): same bake, but the result is
+   written to texels_out[numTexels] (initial values taken from geo->texels, which is not modified).
+   Returns 0 on success, a negative fmgi error code otherwise (no exit()). */
+int getGlobalIlluminationCl(const fmgi_geometry *geo, int numSamplesPerArea, fmgi_vec3 *texels_out);
+
+/* ---- Build-defined device-resident API ---------------------------------------------------------- */
+enum {
+    FMGI_OK = 0,
+    FMGI_ERR_NO_DEVICE = -1,
+    FMGI_ERR_HIP = -2,
+    FMGI_ERR_ARG = -3,
+    FMGI_ERR_STATE = -4,
+    FMGI_ERR_OOM = -5
+};
+
+enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1 };
+
+/* Per-bake counters, accumulated on the device (one atomic per wave). */
+typedef struct fmgi_stats {
+    uint64_t photons;   /* tracePhoton calls                                     */
+    uint64_t scans;     /* rectangle-list scans (photonmap.cl:194)                */
+    uint64_t deposits;  /* lightmap deposits (photonmap.cl:257)                   */
+    uint64_t escapes;   /* scans that hit nothing (photonmap.cl:208)              */
+    uint64_t exact_rescans; /* fast kernel: scans re-done by the exact scan          */
+    uint64_t tests;     /* rectangle tests actually evaluated                      */
+    uint64_t reserved[2];
+} fmgi_stats;
+
+/* One work item of the flattened reference launch schedule (global_illumination_cl.c:246-267). */
+typedef struct fmgi_launch {
+    uint64_t item_begin; /* flattened index of this launch's gid 0 */
+    uint32_t count;      /* workSize                               */
+    int32_t rng_offset;  /* rand() value (kernel arg 4)             */
+    int32_t source;      /* windows first, then lights              */
+    int32_t is_window;   /* kernel arg 5                            */
+} fmgi_launch;
+
+/* One recorded bounce (debug trace mode, for per-photon parity tests). */
+typedef struct fmgi_event {
+    int32_t photon, depth, rect, texel;
+    float rgb[3];
+    uint32_t rng;
+} fmgi_event;
+
+typedef struct fmgi_context fmgi_context;
+
+const char *fmgi_version(void);
+const char *fmgi_last_error(void);
+int fmgi_device_count(void);
+
+/* Create a context on HIP device `device` (hipSetDevice is called). NULL on failure.
+   device == FMGI_HOST_ONLY gives a context without a device: scene checks and fmgi_plan work, every
+   device operation returns FMGI_ERR_NO_DEVICE (used by the CPU test-suite). */
+#define FMGI_HOST_ONLY (-1)
+fmgi_context *fmgi_create(int device);
+void fmgi_destroy(fmgi_context *ctx);
+
+/* Upload the scene: wall rectangles (the rect list scanned by every photon) and the emitters
+   (windows first, then lights). Precomputes the per-rectangle constants on the host in IEEE fp32
+   exactly as photonmap.cl would compute them. */
+int fmgi_set_scene(fmgi_context *ctx, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
+                   int num_windows, const fmgi_rect *lights, int num_lights, int num_texels);
+
+/* Reference launch schedule for spa / wg. If rng_offsets is NULL, libc rand() is called once per
+   launch in reference order; otherwise offsets are taken from rng_offsets[0..n_offsets).
+   Returns the number of launches (>=0) or an error code; *total_items receives the work-item count
+   (photons = 100 * items). The schedule is kept in the context for fmgi_bake_items. */
+int64_t fmgi_plan(fmgi_context *ctx, int spa, int wg, const int32_t *rng_offsets, int64_t n_offsets,
+                  uint64_t *total_items);
+/* Copy the current schedule out (cap entries). Returns the number of launches. */
+int64_t fmgi_get_plan(fmgi_context *ctx, fmgi_launch *out, int64_t cap);
+/* Schedule helpers that do not call rand(). */
+int64_t fmgi_plan_count(const fmgi_rect *windows, int num_windows, const fmgi_rect *lights, int num_lights,
+                        int spa, int wg, uint64_t *total_items);
+
+/* Trace flattened work items [item_begin, item_end) of the planned schedule on `stream`, adding
+   exact fixed-point deposits (int64, units of 2^-25, layout [numTexels][4], .s[3] unused) into the
+   device buffer lm_fx. Asynchronous; the buffer must be zeroed (or hold a previous partial sum). */
+int fmgi_bake_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, void *lm_fx_dev,
+                    int kernel, void *stream);
+/* Device-side finalisation: texels_out[i].c = (float)((double)texels_in[i].c + lm_fx[i].c * 2^-25),
+   .s[3] copied. Either texel pointer may alias. */
+int fmgi_finalize(fmgi_context *ctx, const void *lm_fx_dev, const void *texels_in_dev, void *texels_out_dev,
+                  void *stream);
+/* Counters of all bakes since the last reset (synchronises the context's device). */
+int fmgi_get_stats(fmgi_context *ctx, fmgi_stats *out);
+int fmgi_reset_stats(fmgi_context *ctx);
+/* Debug trace: runs items [item_begin, item_end) (<= 4096 items) with the chosen kernel and returns
+   every bounce in events[(item - item_begin) * 800 + k] (800 = 100 photons x 8 bounces), the number
+   of events per item in counts[], and the final per-item RNG state in rng_final[]. Synchronous. */
+int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, int kernel,
+                     fmgi_event *events, int32_t *counts, uint32_t *rng_final);
+
+/* Host helpers exported for tests (no device needed). */
+void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);
+/* Device-side twin of fmgi_host_sincosf over n inputs (synchronous; for parity tests). */
+int fmgi_device_sincosf(fmgi_context *ctx, const float *x, float *s, float *c, int64_t n);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,53 @@
+#!/usr/bin/env bash
+# oracle/build_ref.sh -- compile the REFERENCE's own sources, in place under /root/reference,
+# into oracle/_ref/ (git-ignored; travels to the GPU box with the snapshot). Test infrastructure only.
+#
+#   _ref/photonmap_strict.hsaco  reference photonmap.cl for gfx950 with ROCm's OpenCL device
+#                                libraries; IEEE div/sqrt (-cl-fp32-correctly-rounded-divide-sqrt),
+#                                no FMA contraction -- the oracle's arithmetic contract.
+#   _ref/photonmap_fast.hsaco    same source with the flags the reference itself passes to
+#                                clBuildProgram (global_illumination_cl.c:196: -cl-fast-relaxed-math).
+#   _ref/dump_geometry           reference parseLayout.c/image.c/png_helper.c/rectangle.c/... +
+#                                oracle/dump_geometry.c; turns a layout PNG into a geometry fixture.
+#   _ref/globalIllumination_fmgi reference main.c + its layout/IO objects linked against OUR
+#                                libflatmatch_gi.so instead of global_illumination_cl.o (drop-in check).
+#
+# No reference file is copied into the repository; nothing here is needed at run time on the GPU box
+# except the built artefacts themselves.
+set -euo pipefail
+REF=${FMGI_REFERENCE:-/root/reference}
+HERE="$(cd "$(dirname "${BASH_SOURCE[0]}")" && pwd)"
+REPO="$(dirname "$HERE")"
+OUT="$HERE/_ref"
+CLANG=${CLANG:-/opt/rocm/lib/llvm/bin/clang}
+mkdir -p "$OUT/obj"
+
+if [ ! -f "$REF/photonmap.cl" ]; then
+    echo "build_ref: $REF not present; skipping reference builds" >&2
+    exit 0
+fi
+
+CLFLAGS="-x cl -cl-std=CL1.2 -Xclang -finclude-default-header -target amdgcn-amd-amdhsa -mcpu=gfx950 -O3"
+$CLANG $CLFLAGS -Wno-nan-infinity-disabled -cl-fp32-correctly-rounded-divide-sqrt -ffp-contract=off "$REF/photonmap.cl" -o "$OUT/photonmap_strict.hsaco"
+$CLANG $CLFLAGS -Wno-nan-infinity-disabled -cl-fast-relaxed-math "$REF/photonmap.cl" -o "$OUT/photonmap_fast.hsaco"
+
+# Host C objects of the reference (flags as in the reference Makefile:21,26 minus -flto/-g).
+PNG_INC=${PNG_INC:-/opt/conda/include}
+PNG_SO=${PNG_SO:-/usr/lib/x86_64-linux-gnu/libpng16.so.16}  # system libpng (same 1.6.37 ABI as the conda headers)
+CFLAGS="-O2 -msse3 -std=c99 -DNDEBUG -DCL_TARGET_OPENCL_VERSION=120 -I$REF -I/opt/rocm/include -I$PNG_INC -w"
+for f in parseLayout image png_helper rectangle geometry vector3_cl helpers photonmap geoSphere radiosityNative main; do
+    gcc $CFLAGS -c "$REF/$f.c" -o "$OUT/obj/$f.o"
+done
+gcc $CFLAGS -c "$HERE/dump_geometry.c" -o "$OUT/obj/dump_geometry.o"
+COMMON="$OUT/obj/parseLayout.o $OUT/obj/image.o $OUT/obj/png_helper.o $OUT/obj/rectangle.o $OUT/obj/geometry.o $OUT/obj/vector3_cl.o $OUT/obj/helpers.o"
+gcc -o "$OUT/dump_geometry" "$OUT/obj/dump_geometry.o" $COMMON "$PNG_SO" -lm
+
+# Drop-in link check: the reference CLI against our C-ABI library (needs the product .so built).
+LIB="$REPO/flatmatch-global-illumination_amd/libflatmatch_gi.so"
+if [ -f "$LIB" ]; then
+    g++ -o "$OUT/globalIllumination_fmgi" "$OUT/obj/main.o" $COMMON "$OUT/obj/photonmap.o" \
+        "$OUT/obj/geoSphere.o" "$OUT/obj/radiosityNative.o" \
+        -L"$(dirname "$LIB")" -Wl,-rpath,'$ORIGIN/../../flatmatch-global-illumination_amd' -lflatmatch_gi \
+        "$PNG_SO" -lm
+fi
+echo "build_ref: OK -> $OUT"

@@ -1,0 +1,186 @@
+"""ctypes wrapper of oracle/liboracle.so -- the CPU ORACLE (TEST INFRASTRUCTURE ONLY).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg import this module, as the
+checker / CPU baseline; the product (libflatmatch_gi.so, fmgi) never does. See fm_oracle.h.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+import subprocess
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+LIB = os.path.join(HERE, "liboracle.so")
+
+LAUNCH_DTYPE = np.dtype(
+    [("item_begin", "<u8"), ("count", "<u4"), ("rng_offset", "<i4"), ("source", "<i4"), ("is_window", "<i4")]
+)
+EVENT_DTYPE = np.dtype(
+    [("photon", "<i4"), ("depth", "<i4"), ("rect", "<i4"), ("texel", "<i4"), ("rgb", "<f4", 3), ("rng", "<u4")]
+)
+
+
+class OracleStats(C.Structure):
+    _fields_ = [(k, C.c_uint64) for k in ("photons", "scans", "deposits", "escapes", "inexact")]
+
+    def as_dict(self):
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+_lib = None
+
+
+def build():
+    subprocess.run(["make", "-s", "-C", HERE], check=True)
+
+
+def load():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB):
+            build()
+        lib = C.CDLL(LIB)
+        vp, i64, u64 = C.c_void_p, C.c_int64, C.c_uint64
+        lib.fmo_schedule_count.restype = i64
+        lib.fmo_schedule_count.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, C.POINTER(u64)]
+        lib.fmo_schedule.restype = i64
+        lib.fmo_schedule.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64]
+        lib.fmo_bake.restype = None
+        lib.fmo_bake.argtypes = [vp, C.c_int, vp, vp, i64, u64, u64, vp, i64, C.c_int, C.POINTER(OracleStats)]
+        lib.fmo_trace_item.restype = C.c_int
+        lib.fmo_trace_item.argtypes = [vp, C.c_int, vp, C.c_int, C.c_uint32, vp, C.c_int, C.POINTER(C.c_uint32)]
+        lib.fmo_trace_item_f32.restype = None
+        lib.fmo_trace_item_f32.argtypes = [vp, C.c_int, vp, C.c_int, C.c_uint32, vp]
+        lib.fmo_rand.restype = C.c_float
+        lib.fmo_rand.argtypes = [C.POINTER(C.c_uint32)]
+        lib.fmo_finalize.restype = None
+        lib.fmo_finalize.argtypes = [vp, i64, vp, vp]
+        _lib = lib
+    return _lib
+
+
+def _p(a):
+    return None if a is None or a.size == 0 else a.ctypes.data_as(C.c_void_p)
+
+
+def schedule(scene, spa: int, wg: int = 256) -> np.ndarray:
+    """global_illumination_cl.c:215-272 schedule; calls libc rand() once per launch."""
+    lib = load()
+    src = np.ascontiguousarray(scene.sources)
+    tot = C.c_uint64()
+    n = lib.fmo_schedule_count(_p(src), len(scene.windows), len(scene.lights), spa, wg, C.byref(tot))
+    out = np.zeros(n, LAUNCH_DTYPE)
+    lib.fmo_schedule(_p(src), len(scene.windows), len(scene.lights), spa, wg, _p(out), n)
+    return out
+
+
+def schedule_with_offsets(scene, spa: int, offsets, wg: int = 256) -> np.ndarray:
+    """Schedule whose launch k uses offsets[k] instead of rand() (item layout as the reference)."""
+    lib = load()
+    src = np.ascontiguousarray(scene.sources)
+    tot = C.c_uint64()
+    n = lib.fmo_schedule_count(_p(src), len(scene.windows), len(scene.lights), spa, wg, C.byref(tot))
+    out = np.zeros(n, LAUNCH_DTYPE)
+    # build the layout in Python (same arithmetic as fmo_schedule minus rand())
+    cap = wg * 100
+    item = 0
+    k = 0
+    f32 = np.float32
+    for s_idx, s in enumerate(scene.sources):
+        w, h = s["width"][:3], s["height"][:3]
+        lw = f32(np.sqrt(f32(f32(f32(w[0] * w[0]) + f32(w[1] * w[1])) + f32(w[2] * w[2]))))
+        lh = f32(np.sqrt(f32(f32(f32(h[0] * h[0]) + f32(h[1] * h[1])) + f32(h[2] * h[2]))))
+        area = f32(lw * lh)
+        nitems = int(f32(f32(f32(spa) * area) / f32(100)))
+        nitems = (nitems // wg + 1) * wg
+        while nitems:
+            ws = min(nitems, cap)
+            nitems -= ws
+            out[k] = (item, ws, int(offsets[k]), s_idx, int(s_idx < len(scene.windows)))
+            item += ws
+            k += 1
+    assert k == n and item == tot.value
+    return out
+
+
+def bake(scene, launches: np.ndarray, item_begin: int = 0, item_end: int | None = None, nthreads: int = 0):
+    """Exact fixed-point lightmap (int64 [numTexels, 3], units of 2^-25) of items [begin, end)."""
+    lib = load()
+    if item_end is None:
+        item_end = int(launches["item_begin"][-1] + launches["count"][-1])
+    walls = np.ascontiguousarray(scene.walls)
+    src = np.ascontiguousarray(scene.sources)
+    L = np.ascontiguousarray(launches, LAUNCH_DTYPE)
+    lm = np.zeros((scene.num_texels, 3), np.int64)
+    st = OracleStats()
+    lib.fmo_bake(_p(walls), len(walls), _p(src), _p(L), len(L), item_begin, item_end, _p(lm), scene.num_texels,
+                 nthreads, C.byref(st))
+    return lm, st.as_dict()
+
+
+def trace_item(scene, source: int, is_window: int, rng_state: int, cap: int = 800):
+    lib = load()
+    walls = np.ascontiguousarray(scene.walls)
+    src = np.ascontiguousarray(scene.sources[source : source + 1])
+    ev = np.zeros(cap, EVENT_DTYPE)
+    fin = C.c_uint32()
+    n = lib.fmo_trace_item(_p(walls), len(walls), _p(src), is_window, rng_state & 0xFFFFFFFF, _p(ev), cap, C.byref(fin))
+    return ev[: min(n, cap)], int(fin.value)
+
+
+def trace_item_f32(scene, source: int, is_window: int, rng_state: int) -> np.ndarray:
+    lib = load()
+    walls = np.ascontiguousarray(scene.walls)
+    src = np.ascontiguousarray(scene.sources[source : source + 1])
+    tex = np.zeros((scene.num_texels, 4), np.float32)
+    lib.fmo_trace_item_f32(_p(walls), len(walls), _p(src), is_window, rng_state & 0xFFFFFFFF, _p(tex))
+    return tex
+
+
+def finalize(lm_fx: np.ndarray, texels_in: np.ndarray) -> np.ndarray:
+    lib = load()
+    lm = np.ascontiguousarray(lm_fx, np.int64)
+    tin = np.ascontiguousarray(texels_in, np.float32)
+    out = np.empty_like(tin)
+    lib.fmo_finalize(_p(lm), len(tin), _p(tin), _p(out))
+    return out
+
+
+def rand_sequence(state: int, n: int) -> np.ndarray:
+    lib = load()
+    s = C.c_uint32(state)
+    return np.array([lib.fmo_rand(C.byref(s)) for _ in range(n)], np.float32)
+
+
+# ---- the reference kernel itself (GPU only): oracle/_ref/photonmap_*.hsaco via libref_runner.so ----
+REF_DIR = os.path.join(HERE, "_ref")
+_ref = None
+
+
+def ref_kernel_available(variant: str = "strict") -> bool:
+    return os.path.exists(os.path.join(REF_DIR, f"photonmap_{variant}.hsaco")) and os.path.exists(
+        os.path.join(HERE, "libref_runner.so"))
+
+
+def ref_run_items(scene, source: int, is_window: int, rng_states, variant: str = "strict") -> np.ndarray:
+    """Run the reference photonmap kernel (photonmap.cl:269) once per work item, each on a zeroed
+    lightColors buffer; returns float32 [n, numTexels, 4]."""
+    global _ref
+    if _ref is None:
+        _ref = C.CDLL(os.path.join(HERE, "libref_runner.so"))
+        _ref.ref_open.argtypes = [C.c_char_p]
+        _ref.ref_last_error.restype = C.c_char_p
+        _ref.ref_run_items.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                       C.c_void_p]
+    path = os.path.join(REF_DIR, f"photonmap_{variant}.hsaco")
+    if _ref.ref_open(path.encode()) != 0:
+        raise RuntimeError(_ref.ref_last_error().decode())
+    walls = np.ascontiguousarray(scene.walls)
+    win = np.ascontiguousarray(scene.sources[source : source + 1])
+    rs = np.ascontiguousarray(rng_states, np.uint32)
+    out = np.zeros((len(rs), scene.num_texels, 4), np.float32)
+    if _ref.ref_run_items(_p(win), _p(walls), len(walls), scene.num_texels, is_window, _p(rs), len(rs), _p(out)) != 0:
+        raise RuntimeError(_ref.ref_last_error().decode())
+    return out

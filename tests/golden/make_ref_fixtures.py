@@ -1,0 +1,83 @@
+"""Pin the oracle against the REFERENCE KERNEL ITSELF (run on the GPU box; outputs are committed).
+
+The reference's photonmap.cl, compiled for gfx950 by oracle/build_ref.sh with ROCm's OpenCL device
+libraries, is launched one work item at a time on a zeroed lightColors buffer (oracle/ref_runner.cpp;
+one item per launch removes the kernel's data race, photonmap.cl:256). Each item's fp32 lightmap is
+stored sparsely as a fixture and compared with the oracle's fp32 per-item sum (fm_oracle.trace_item_f32):
+
+  ref_items_<scene>_<variant>.npz : rng_state[n], source, is_window, and for every item the non-zero
+                                    texel indices and their float4 values (reference kernel output)
+
+variant "strict": -cl-fp32-correctly-rounded-divide-sqrt -ffp-contract=off (IEEE, the oracle contract)
+variant "fast"  : -cl-fast-relaxed-math, the reference's own clBuildProgram flags
+                  (global_illumination_cl.c:196) -- quantifies how far the as-deployed reference is
+                  from any exact restatement.
+Prints a JSON summary (items bit-identical to the oracle, max relative texel difference).
+"""
+import json
+import os
+import sys
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+REPO = os.path.dirname(os.path.dirname(HERE))
+sys.path[:0] = [os.path.join(REPO, "oracle"), os.path.join(REPO, "flatmatch-global-illumination_amd")]
+
+import fm_oracle as O  # noqa: E402
+from fmgi import scene as S  # noqa: E402
+
+
+def run(sc, L, li, gids, variant):
+    src, isw = int(L[li]["source"]), int(L[li]["is_window"])
+    states = np.array([(g + int(L[li]["rng_offset"])) & 0xFFFFFFFF for g in gids], np.uint32)
+    ref = O.ref_run_items(sc, src, isw, states, variant)
+    idx, vals, bounds = [], [], [0]
+    same, maxrel = 0, 0.0
+    for k, st in enumerate(states):
+        nz = np.nonzero(ref[k].any(axis=1))[0]
+        idx.append(nz)
+        vals.append(ref[k][nz])
+        bounds.append(bounds[-1] + len(nz))
+        mine = O.trace_item_f32(sc, src, isw, int(st))
+        if np.array_equal(mine.view(np.uint32), ref[k].view(np.uint32)):
+            same += 1
+        tot_m, tot_r = mine[:, :3].sum(), ref[k][:, :3].sum()
+        maxrel = max(maxrel, abs(float(tot_m) - float(tot_r)) / max(float(tot_r), 1e-30))
+    return dict(rng_state=states, source=src, is_window=isw, bounds=np.array(bounds, np.int64),
+                texel=np.concatenate(idx).astype(np.int32), value=np.concatenate(vals).astype(np.float32)), same, maxrel
+
+
+def main():
+    offs = np.load(os.path.join(HERE, "glibc_rand_4096.npy"))
+    out_dir = sys.argv[1] if len(sys.argv) > 1 else HERE
+    summary = {}
+    cases = [
+        ("example", S.load_geometry(os.path.join(HERE, "example_geometry.bin"), "example"), 65_000,
+         [(0, range(0, 96)), (7, range(0, 32))]),
+        ("box200", S.box_scene(200), 172_413_793, [(0, range(1000, 1048))]),
+    ]
+    for name, sc, spa, parts in cases:
+        L = O.schedule_with_offsets(sc, spa, offs)
+        for variant in ("strict", "fast"):
+            acc = {}
+            n_same = n_tot = 0
+            worst = 0.0
+            for li, gids in parts:
+                d, same, maxrel = run(sc, L, li, list(gids), variant)
+                for k, v in d.items():
+                    acc.setdefault(k, []).append(v)
+                n_same += same
+                n_tot += len(gids)
+                worst = max(worst, maxrel)
+            np.savez_compressed(os.path.join(out_dir, f"ref_items_{name}_{variant}.npz"),
+                                **{f"{k}_{i}": v for k, vs in acc.items() for i, v in enumerate(vs)})
+            summary[f"{name}/{variant}"] = {"items": n_tot, "bit_identical_to_oracle": n_same,
+                                            "max_rel_item_total_diff": worst}
+    print(json.dumps(summary, indent=1))
+    with open(os.path.join(out_dir, "ref_items_summary.json"), "w") as f:
+        json.dump(summary, f, indent=1)
+
+
+if __name__ == "__main__":
+    main()
