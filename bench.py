@@ -92,6 +92,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state"])
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -117,6 +118,7 @@ def main():
     kernel = fmgi.KERNEL_FAST if args.kernel == "fast" else fmgi.KERNEL_EXACT
 
     ctx = fmgi.Context(local)
+    ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE}[args.accum])
     ctx.set_scene(sc)
     libc = ctypes.CDLL(None)
     libc.srand(1)  # the unseeded state main.c runs with; every rank builds the same schedule
@@ -126,11 +128,14 @@ def main():
     photons_per_step = 100 * total_items
 
     dev = torch.device("cuda", local)
+    # one non-default stream for every device op of the step: the lightmap zero-fill, the bake kernel,
+    # the RCCL reduce (ordered after it by torch) and the finalisation; HIP events time the bake on it
+    stream = torch.cuda.Stream(device=dev)
+    torch.cuda.set_stream(stream)
+    sptr = stream.cuda_stream
     lm = torch.zeros((sc.num_texels, 4), dtype=torch.int64, device=dev)
     tex_in = torch.zeros((sc.num_texels, 4), dtype=torch.float32, device=dev)
     tex_out = torch.empty_like(tex_in)
-    stream = torch.cuda.current_stream()
-    sptr = stream.cuda_stream
 
     k_ms = []
 
@@ -208,6 +213,7 @@ def main():
                 "spa": spa,
                 "photons_per_step": photons_per_step,
                 "kernel": args.kernel,
+                "accumulation": {1: "fx3", 2: "state"}[ctx.accumulation],
                 "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
             },
             "roofline": {

@@ -101,6 +101,120 @@ uint64_t source_items(const fmgi_rect &src, float spa, uint64_t wg) {
     return (n / wg + 1) * wg;
 }
 
+/*
+ * Filter tables for ScanFast (fmgi_kernels.hip). A rect is "axis-aligned" when its normal, width and
+ * height each have exactly one non-zero component, on three different axes: then photonmap.cl's dot
+ * products reduce to one product each and the phase-1 value fac' = (plane - src_a) * rcp(dir_a) is within
+ * 2^-20 relative of the exact fac. The extent along u/v is grown by a margin M that bounds every other
+ * phase-1 vs exact difference for a hit inside the scene's bounding box (distance <= diagonal D,
+ * coordinates <= S): |d| * |fac' - fac| <= D * 2^-20 plus a few ulps of S and D from the exact
+ * ray/pDir/dot roundings and the phase-1 fma; M = max(S, D) * 2^-17 covers all of it with >= 4x slack.
+ */
+struct FilterBuild {
+    std::vector<FilterRec> img; /* per axis a: J[a] pairs {+a record j, -a record j} */
+    int J[3] = {0, 0, 0};
+    std::vector<int32_t> general;
+    float margin = 0;
+};
+
+int nonzero_axis(const float *v) {
+    int axis = -1;
+    for (int k = 0; k < 3; k++) {
+        if (v[k] != 0.0f) {
+            if (axis >= 0) return -1;
+            axis = k;
+        }
+    }
+    return axis;
+}
+
+FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, int ns) {
+    FilterBuild fb;
+    double lo[3] = {1e300, 1e300, 1e300}, hi[3] = {-1e300, -1e300, -1e300};
+    auto grow = [&](const fmgi_rect &r) {
+        for (int cs = 0; cs < 4; cs++) {
+            for (int k = 0; k < 3; k++) {
+                double x = (double)r.pos.s[k] + ((cs & 1) ? (double)r.width.s[k] : 0.0) +
+                           ((cs & 2) ? (double)r.height.s[k] : 0.0);
+                lo[k] = std::min(lo[k], x);
+                hi[k] = std::max(hi[k], x);
+            }
+        }
+    };
+    for (int i = 0; i < nw; i++) grow(walls[i]);
+    for (int i = 0; i < ns; i++) grow(srcs[i]);
+    double S = 0, D2 = 0;
+    for (int k = 0; k < 3; k++) {
+        if (nw + ns == 0) break;
+        S = std::max(S, std::max(fabs(lo[k]), fabs(hi[k])));
+        D2 += (hi[k] - lo[k]) * (hi[k] - lo[k]);
+    }
+    double B = std::max(std::max(S, sqrt(D2)), 1.0);
+    fb.margin = (float)(B * (1.0 / 131072.0));
+    std::vector<FilterRec> cls[3][2];
+    for (int i = 0; i < nw; i++) {
+        const fmgi_rect &r = walls[i];
+        int a = nonzero_axis(r.n.s), aw = nonzero_axis(r.width.s), ah = nonzero_axis(r.height.s);
+        if (a < 0 || aw < 0 || ah < 0 || aw == a || ah == a || aw == ah) {
+            fb.general.push_back(i);
+            continue;
+        }
+        int u = (a == 0) ? 1 : 0, v = (a == 2) ? 1 : 2;
+        double e_lo[3], e_hi[3];
+        for (int k = 0; k < 3; k++) {
+            double p0 = r.pos.s[k], p1 = p0 + (double)r.width.s[k] + (double)r.height.s[k];
+            e_lo[k] = std::min(p0, p1);
+            e_hi[k] = std::max(p0, p1);
+        }
+        FilterRec f;
+        memset(&f, 0, sizeof f);
+        f.plane = r.pos.s[a];
+        f.cu = (float)((e_lo[u] + e_hi[u]) * 0.5);
+        f.hwu = (float)((e_hi[u] - e_lo[u]) * 0.5 + fb.margin);
+        f.cv = (float)((e_lo[v] + e_hi[v]) * 0.5);
+        f.hwv = (float)((e_hi[v] - e_lo[v]) * 0.5 + fb.margin);
+        f.idx = i;
+        cls[a][r.n.s[a] > 0 ? 0 : 1].push_back(f);
+    }
+    FilterRec sentinel;
+    memset(&sentinel, 0, sizeof sentinel);
+    sentinel.hwu = -1.0f; /* |x| <= -1 is never true: a padding entry is never a candidate */
+    sentinel.hwv = -1.0f;
+    sentinel.idx = -1;
+    for (int a = 0; a < 3; a++) {
+        fb.J[a] = (int)std::max(cls[a][0].size(), cls[a][1].size());
+        for (int j = 0; j < fb.J[a]; j++)
+            for (int c = 0; c < 2; c++)
+                fb.img.push_back(j < (int)cls[a][c].size() ? cls[a][c][j] : sentinel);
+    }
+    if (fb.img.empty()) fb.img.push_back(sentinel);
+    return fb;
+}
+
+/* Exact deposit colour of every colour state (kernel: k_bake's `sid`), in fixed point. The float ops
+   replay photonmap.cl:167-169,241-249 in the kernel's order, so the values are bit-identical. */
+std::vector<long long> colour_table() {
+    std::vector<long long> t((size_t)FMGI_COLOUR_STATES * 3, 0);
+    for (int sid = 0; sid < FMGI_COLOUR_STATES; sid++) {
+        int s = sid & 511;
+        if (s == 0) continue;
+        f3 c = (sid & 512) ? mkf3(18, 18, 18) : mkf3(16, 16, 18);
+        int nb = 0;
+        while ((s >> (nb + 1)) != 0) nb++; /* bits below the leading 1 = diffuse bounces */
+        for (int b = nb - 1; b >= 0; b--) {
+            if ((s >> b) & 1) {
+                c.y *= 0.85f;
+                c.z *= 0.7f;
+            }
+            c = mul3(c, 0.9f);
+        }
+        t[3 * sid + 0] = (long long)ldexp((double)c.x, FMGI_FX_SHIFT);
+        t[3 * sid + 1] = (long long)ldexp((double)c.y, FMGI_FX_SHIFT);
+        t[3 * sid + 2] = (long long)ldexp((double)c.z, FMGI_FX_SHIFT);
+    }
+    return t;
+}
+
 } // namespace
 
 struct fmgi_context {
@@ -119,6 +233,18 @@ struct fmgi_context {
     uint64_t total_items = 0;
     unsigned long long *d_counter = nullptr;
     unsigned long long *d_stats = nullptr;
+    /* ScanFast filter image + non-axis-aligned rect list */
+    FilterRec *d_fimg = nullptr;
+    int fimg_bytes = 0;
+    int32_t *d_general = nullptr;
+    int fJ[3] = {0, 0, 0};
+    int ngeneral = 0;
+    float margin = 0;
+    /* accumulation: FMGI_ACCUM_FX3 or FMGI_ACCUM_STATE (counts[1024][numTexels] + colour table) */
+    int accum_req = FMGI_ACCUM_AUTO;
+    int accum = FMGI_ACCUM_FX3;
+    unsigned int *d_counts = nullptr;
+    long long *d_colfx = nullptr;
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -180,11 +306,47 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_rects);
     hipFree(c->d_srcs);
     hipFree(c->d_launches);
+    hipFree(c->d_fimg);
+    hipFree(c->d_general);
+    hipFree(c->d_counts);
+    hipFree(c->d_colfx);
     hipFree(c->d_counter);
     hipFree(c->d_stats);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
+
+/* AccState needs 4 KiB of counters per texel; above this budget (or on request) AccFx3 is used. */
+static const size_t kStateBudget = (size_t)4 << 30;
+
+static int configure_accum(fmgi_context *c) {
+    size_t bytes = (size_t)FMGI_COLOUR_STATES * (size_t)c->num_texels * sizeof(unsigned int);
+    int want = c->accum_req;
+    if (want == FMGI_ACCUM_AUTO) want = (bytes && bytes <= kStateBudget) ? FMGI_ACCUM_STATE : FMGI_ACCUM_FX3;
+    hipFree(c->d_counts);
+    c->d_counts = nullptr;
+    c->accum = FMGI_ACCUM_FX3;
+    if (want != FMGI_ACCUM_STATE || !bytes) return FMGI_OK;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMalloc(&c->d_counts, bytes));
+    HIPCHK(hipMemset(c->d_counts, 0, bytes));
+    if (!c->d_colfx) {
+        std::vector<long long> t = colour_table();
+        HIPCHK(hipMalloc(&c->d_colfx, t.size() * sizeof(long long)));
+        HIPCHK(hipMemcpy(c->d_colfx, t.data(), t.size() * sizeof(long long), hipMemcpyHostToDevice));
+    }
+    c->accum = FMGI_ACCUM_STATE;
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_set_accumulation(fmgi_context *c, int mode) {
+    if (!c || mode < FMGI_ACCUM_AUTO || mode > FMGI_ACCUM_STATE) return set_err(FMGI_ERR_ARG, "bad accumulation mode");
+    c->accum_req = mode;
+    if (c->device == FMGI_HOST_ONLY || c->num_texels == 0) return FMGI_OK;
+    return configure_accum(c);
+}
+
+FMGI_API int fmgi_get_accumulation(fmgi_context *c) { return c ? c->accum : set_err(FMGI_ERR_ARG, "null context"); }
 
 FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
                             int num_windows, const fmgi_rect *lights, int num_lights, int num_texels) {
@@ -204,6 +366,11 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->h_srcs.clear();
     for (int i = 0; i < num_windows; i++) { sd.push_back(make_src(windows[i])); c->h_srcs.push_back(windows[i]); }
     for (int i = 0; i < num_lights; i++) { sd.push_back(make_src(lights[i])); c->h_srcs.push_back(lights[i]); }
+    FilterBuild fb = build_filter(walls, num_walls, c->h_srcs.data(), (int)c->h_srcs.size());
+    for (int a = 0; a < 3; a++) c->fJ[a] = fb.J[a];
+    c->fimg_bytes = (int)(fb.img.size() * sizeof(FilterRec));
+    c->ngeneral = (int)fb.general.size();
+    c->margin = fb.margin;
     if (c->device != FMGI_HOST_ONLY) {
     HIPCHK(hipSetDevice(c->device));
     hipFree(c->d_rects);
@@ -218,6 +385,21 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
         HIPCHK(hipMalloc(&c->d_srcs, sd.size() * sizeof(SrcDev)));
         HIPCHK(hipMemcpy(c->d_srcs, sd.data(), sd.size() * sizeof(SrcDev), hipMemcpyHostToDevice));
     }
+    hipFree(c->d_fimg);
+    hipFree(c->d_general);
+    c->d_fimg = nullptr;
+    c->d_general = nullptr;
+    HIPCHK(hipMalloc(&c->d_fimg, fb.img.size() * sizeof(FilterRec)));
+    HIPCHK(hipMemcpy(c->d_fimg, fb.img.data(), fb.img.size() * sizeof(FilterRec), hipMemcpyHostToDevice));
+    if (!fb.general.empty()) {
+        HIPCHK(hipMalloc(&c->d_general, fb.general.size() * sizeof(int32_t)));
+        HIPCHK(hipMemcpy(c->d_general, fb.general.data(), fb.general.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    }
+    c->num_texels = num_texels;
+    if (c->device != FMGI_HOST_ONLY) {
+        int rc = configure_accum(c);
+        if (rc != FMGI_OK) return rc;
     }
     c->nrects = num_walls;
     c->nsrcs = num_windows + num_lights;
@@ -326,11 +508,28 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.counter = c->d_counter;
     a.lm = (unsigned long long *)lm;
     a.stats = c->d_stats;
+    a.fimg = c->d_fimg;
+    a.fimg_bytes = c->fimg_bytes;
+    for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
+    a.general = c->d_general;
+    a.ngeneral = c->ngeneral;
+    a.counts = c->accum == FMGI_ACCUM_STATE ? c->d_counts : nullptr;
+    a.num_texels = c->num_texels;
     a.events = events;
     a.ev_counts = counts;
     a.rng_final = rngf;
-    HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
-    HIPCHK(fmgi_launch_bake(a, kernel, trace, grid_blocks(c, e - b), s));
+    /* AccState: u32 counters must not overflow -> at most 5e6 work items (5e8 photons, <= 4e9
+       deposits) per chunk, each chunk folded into the int64 lightmap (and the counters re-zeroed) */
+    const uint64_t chunk = a.counts ? (uint64_t)5000000 : (e - b);
+    for (uint64_t cb = b; cb < e; cb += chunk) {
+        const uint64_t ce = std::min(e, cb + chunk);
+        a.item_begin = cb;
+        a.item_end = ce;
+        HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
+        HIPCHK(fmgi_launch_bake(a, kernel, trace, grid_blocks(c, ce - cb), 256, s));
+        if (a.counts)
+            HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
+    }
     return FMGI_OK;
 }
 

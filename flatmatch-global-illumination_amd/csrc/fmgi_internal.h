@@ -10,6 +10,16 @@
 
 #include "fmgi_core.h"
 
+/* One axis-aligned rectangle as the conservative filter sees it (32 B = one s_load_dwordx8):
+   the plane coordinate along its normal's axis a, and centre / half-extent (+ margin) along the two
+   other axes u < v. idx = index in the rect list (the exact data is in RectDev[idx]). */
+struct FilterRec {
+    float plane, cu, hwu, cv, hwv;
+    int32_t idx;
+    float pad0, pad1;
+};
+static_assert(sizeof(FilterRec) == 32, "FilterRec must be 32 B");
+
 struct BakeArgs {
     const RectDev *rects;
     int nrects;
@@ -20,9 +30,17 @@ struct BakeArgs {
     unsigned long long *counter;   /* work-item fetch counter, zeroed before each bake */
     unsigned long long *lm;        /* int64 fixed point [numTexels][4]                   */
     unsigned long long *stats;     /* fmgi_stats words                                   */
-    /* fast-kernel filter parameters (fmgi_kernels.hip, "conservative filter") */
-    int axis_begin[7];             /* rects sorted by axis class: [axis_begin[c], axis_begin[c+1]) */
-    float eps_abs;                 /* absolute slack of the filter (scene-scale dependent)          */
+    /* fast-kernel filter (fmgi_kernels.hip, ScanFast): the LDS image = for each axis a, fJ[a] pairs of
+       FilterRec {+a class record j, -a class record j} (64 B per pair; the shorter class is padded with
+       never-valid sentinels). Rects that are not axis-aligned are listed in `general`. */
+    const void *fimg;
+    int fimg_bytes;
+    int fJ[3];
+    const int32_t *general;
+    int ngeneral;
+    /* AccState accumulation: u32 counts[FMGI_COLOUR_STATES][num_texels] (NULL -> AccFx3) */
+    unsigned int *counts;
+    int num_texels;
     /* debug trace (TRACE kernels only) */
     void *events;                  /* fmgi_event[(item - item_begin) * 800 + k]                     */
     int32_t *ev_counts;
@@ -31,10 +49,13 @@ struct BakeArgs {
 
 enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESCANS, KSTAT_TESTS, KSTAT_N = 8 };
 
-hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, bool trace, int grid_blocks, hipStream_t s);
+#define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
+
+hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, bool trace, int grid_blocks, int block, hipStream_t s);
+hipError_t fmgi_launch_reduce_states(unsigned int *counts, const long long *colfx, unsigned long long *lm, int n,
+                                     hipStream_t s);
 hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, float *tout, int64_t n,
                                 hipStream_t s);
 hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, hipStream_t s);
-int fmgi_block_size();
 
 #endif

@@ -7,10 +7,12 @@
  *     one at once and the grid is persistent (no per-launch tail, no 25,600-item launches);
  *   - the photon/bounce loops are flattened per lane (a lane whose photon escapes starts its next
  *     photon in the same loop iteration);
- *   - the rectangle list is wave-uniform: every lane tests rect i at the same time, so the rect
- *     record is read with scalar loads into SGPRs (no VGPR/LDS traffic per test);
- *   - deposits go to an int64 fixed-point lightmap with device-scope atomics: exact, race-free and
- *     order-independent (the reference's lightColors[] += is a data race, photonmap.cl:256).
+ *   - wave-uniform data (rect records of the exact scan) is read through the constant address space,
+ *     i.e. scalar loads into SGPRs; the fast scan's filter records are staged in LDS once per
+ *     workgroup and read per lane (each lane reads the record of the class it faces);
+ *   - deposits are exact and order-free: either three int64 fixed-point atomics per deposit (AccFx3)
+ *     or one u32 counter per (colour state, texel) (AccState) folded into int64 by k_reduce_states.
+ *     The reference's lightColors[] += is a data race (photonmap.cl:256); these are not.
  * Two scan policies share the state machine: ScanExact (photonmap.cl:194-206 literally) and
  * ScanFast (conservative fp32 filter + exact verification; identical results, see below).
  */
@@ -23,6 +25,9 @@
 #endif
 
 namespace {
+
+template <class T>
+using cptr = const __attribute__((address_space(4))) T *; /* constant space: scalar loads */
 
 struct LcgJumpC {
     uint32_t a[41], c[41];
@@ -65,19 +70,31 @@ __device__ __forceinline__ unsigned long long wave_sum(unsigned long long v) {
     return v;
 }
 
+__device__ __forceinline__ float exact_on(cptr<RectDev> R, int i, f3 src, f3 dir, float closest) {
+    const float nx = R[i].nx, ny = R[i].ny, nz = R[i].nz, px = R[i].px, py = R[i].py, pz = R[i].pz;
+    const float wx = R[i].wnx, wy = R[i].wny, wz = R[i].wnz, wl = R[i].wl;
+    const float hx = R[i].hnx, hy = R[i].hny, hz = R[i].hnz, hl = R[i].hl;
+    return intersect_exact(mkf3(nx, ny, nz), mkf3(px, py, pz), mkf3(wx, wy, wz), wl, mkf3(hx, hy, hz), hl, src,
+                           dir, closest);
+}
+
+__device__ __forceinline__ float exact_at(const RectDev &r, f3 src, f3 dir, float closest) {
+    return intersect_exact(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz), mkf3(r.wnx, r.wny, r.wnz), r.wl,
+                           mkf3(r.hnx, r.hny, r.hnz), r.hl, src, dir, closest);
+}
+
 /* ---- scan policies -------------------------------------------------------------------------- */
 
 /* photonmap.cl:189-206, evaluated literally for every rectangle in index order. */
 struct ScanExact {
-    static __device__ __forceinline__ int scan(const BakeArgs &a, f3 src, f3 dir, float &best,
+    static constexpr bool kLds = false;
+    static __device__ __forceinline__ int scan(const BakeArgs &a, const char *, f3 src, f3 dir, float &best,
                                                unsigned long long &tests, unsigned long long &) {
-        const RectDev *__restrict__ R = a.rects;
+        cptr<RectDev> R = (cptr<RectDev>)a.rects;
         float bestd = INFINITY;
         int hit = -1;
         for (int i = 0; i < a.nrects; i++) {
-            const RectDev &r = R[i];
-            float d = intersect_exact(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz), mkf3(r.wnx, r.wny, r.wnz),
-                                      r.wl, mkf3(r.hnx, r.hny, r.hnz), r.hl, src, dir, bestd);
+            const float d = exact_on(R, i, src, dir, bestd);
             if (d < 0) continue;
             if (d < bestd) { bestd = d; hit = i; }
         }
@@ -87,13 +104,132 @@ struct ScanExact {
     }
 };
 
+/*
+ * ScanFast: same result as ScanExact, bit for bit, at a fraction of the VALU work.
+ *
+ * Why it is exact (DESIGN.md §Fast scan): let V be the rects passing photonmap.cl's order-independent
+ * tests (front face, fac >= 0, hit point inside both extents). The sequential scan returns the rect m
+ * with the smallest exact fac whenever every other member of V has fac > fac_m * (1 + 2^-13): m is then
+ * accepted whatever was accepted before it (the `closest^2 < |ray|^2` early-out cannot fire for it), and
+ * nothing after it can replace it. Phase 1 evaluates, for every rect, a conservative approximation
+ * (superset of V, fac' within 2^-20 relative of the exact fac); phase 2 evaluates photonmap.cl's
+ * intersects() exactly for the phase-1 winner and checks the separation against the runner-up. Any doubt
+ * (runner-up too close, winner not exactly valid) falls back to the literal exact scan.
+ *
+ * Phase 1 for an axis-aligned rect with normal axis a (all rects of the reference's layouts and of the
+ * synthetic boxes): fac' = (plane - src_a) * rcp(dir_a), hit = src + dir*fac' on the two other axes,
+ * inside the rect's extent grown by a scene-scale margin (host: fmgi_api.cpp build_filter). The filter
+ * image in LDS holds, per axis, pairs {record j of the +a class, record j of the -a class} (64 B); a
+ * lane reads the half of the pair whose class it faces (front face <=> n_a * dir_a < 0), so every lane
+ * spends iteration j on a front-facing rect and no lane needs a select.
+ */
+template <int A>
+__device__ __forceinline__ float comp(f3 v) { return A == 0 ? v.x : (A == 1 ? v.y : v.z); }
+
+template <int A>
+__device__ __forceinline__ void filter_axis(const char *img, int J, f3 s, f3 d, float &L1, float &L2, int &code1) {
+    constexpr int U = (A == 0) ? 1 : 0;
+    constexpr int V = (A == 2) ? 1 : 2;
+    const float sa = comp<A>(s), da = comp<A>(d);
+    const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
+    const float rd = __builtin_amdgcn_rcpf(da);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 32), 16);
+#pragma unroll 4
+    for (int j = 0; j < J; j++) {
+        const float4 q = p[4 * j];                      /* plane, cu, hwu, cv: ds_read_b128 */
+        const float hwv = ((const float *)(p + 4 * j))[4]; /* hwv: ds_read_b32               */
+        const float f = (q.x - sa) * rd;
+        const float uu = fmaf(du, f, su) - q.y;
+        const float vv = fmaf(dv, f, sv) - q.w;
+        const int ok = (int)(f >= 0.0f) & (int)(fabsf(uu) <= q.z) & (int)(fabsf(vv) <= hwv);
+        const float key = ok ? f : INFINITY;
+        const bool lt = key < L1;
+        L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+        code1 = lt ? ((A << 16) | j) : code1;
+        L1 = lt ? key : L1;
+    }
+}
+
+struct ScanFast {
+    static constexpr bool kLds = true;
+    static __device__ __forceinline__ int scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best,
+                                               unsigned long long &tests, unsigned long long &rescans) {
+        float L1 = INFINITY, L2 = INFINITY;
+        int code1 = -1;
+        filter_axis<0>(lds, a.fJ[0], src, dir, L1, L2, code1);
+        filter_axis<1>(lds + 64 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1);
+        filter_axis<2>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1);
+        /* rects that are not axis-aligned: exact order-independent tests (no early-out) */
+        cptr<RectDev> R = (cptr<RectDev>)a.rects;
+        cptr<int32_t> G = (cptr<int32_t>)a.general;
+        for (int g = 0; g < a.ngeneral; g++) {
+            const float f = exact_on(R, G[g], src, dir, INFINITY);
+            const float key = (f < 0) ? INFINITY : f;
+            const bool lt = key < L1;
+            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+            code1 = lt ? ((3 << 16) | g) : code1;
+            L1 = lt ? key : L1;
+        }
+        tests += (unsigned long long)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
+        if (L1 == INFINITY) { /* V is a subset of the (empty) phase-1 set: the photon escapes */
+            best = INFINITY;
+            return -1;
+        }
+        /* phase 2: exact photonmap.cl intersects() of the winner */
+        const int A = code1 >> 16, j = code1 & 0xFFFF;
+        int idx;
+        if (A == 3) {
+            idx = a.general[j];
+        } else {
+            const float dA = A == 0 ? dir.x : (A == 1 ? dir.y : dir.z);
+            const int off = A == 0 ? 0 : (A == 1 ? 64 * a.fJ[0] : 64 * (a.fJ[0] + a.fJ[1]));
+            idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
+        }
+        const float f = exact_at(a.rects[idx], src, dir, INFINITY);
+        /* separation: the runner-up's phase-1 value must exceed the exact winner by > 2^-12 relative
+           (covers the 2^-20 phase-1 error and the 2^-13 early-out slack); false for f = INF */
+        if (!(f < 0) && L2 > f * 1.000244140625f) {
+            best = f;
+            return idx;
+        }
+        rescans++;
+        return ScanExact::scan(a, lds, src, dir, best, tests, rescans);
+    }
+};
+
+/* ---- accumulation policies -------------------------------------------------------------------- */
+
+/* three exact int64 fixed-point atomics per deposit into lm[texel][0..2] */
+struct AccFx3 {
+    static __device__ __forceinline__ void deposit(const BakeArgs &a, int texel, int, f3 col) {
+        unsigned long long *t = a.lm + 4 * (size_t)texel;
+        atomicAdd(t + 0, fx(col.x));
+        atomicAdd(t + 1, fx(col.y));
+        atomicAdd(t + 2, fx(col.z));
+    }
+};
+
+/* one u32 count per (colour state, texel): the deposited colour is a function of the state
+   (source kind + the floor/non-floor sequence of diffuse bounces, see k_reduce_states) */
+struct AccState {
+    static __device__ __forceinline__ void deposit(const BakeArgs &a, int texel, int sid, f3) {
+        atomicAdd(a.counts + (size_t)sid * a.num_texels + texel, 1u);
+    }
+};
+
 /* ---- the per-lane photon state machine ------------------------------------------------------- */
 
-template <class Scan, bool TRACE>
-__global__ __launch_bounds__(256) void k_bake(BakeArgs a) {
+template <class Scan, class Acc, bool TRACE>
+__global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
+    extern __shared__ __attribute__((aligned(16))) char s_img[];
+    if (Scan::kLds) { /* stage the filter image once per workgroup */
+        const int n16 = a.fimg_bytes >> 4;
+        for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
+        __syncthreads();
+    }
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
-    int depth = 0, left = 0, photon = -1;
+    int depth = 0, left = 0, photon = -1, sid = 0;
     int srci = 0;
     bool win = false, alive = false;
     uint64_t item = 0;
@@ -125,6 +261,7 @@ __global__ __launch_bounds__(256) void k_bake(BakeArgs a) {
             /* photonmap.cl:167-181: emission */
             const SrcDev &S = a.srcs[srci];
             col = win ? mkf3(18, 18, 18) : mkf3(16, 16, 18);
+            sid = win ? (512 + 1) : 1; /* colour state: source kind, then one bit per diffuse bounce */
             float dx = rng_next(rng);
             float dy = rng_next(rng);
             dir = sample_dir(rng, mkf3(S.nx, S.ny, S.nz), mkf3(S.bux, S.buy, S.buz), mkf3(S.bvx, S.bvy, S.bvz), win);
@@ -138,7 +275,7 @@ __global__ __launch_bounds__(256) void k_bake(BakeArgs a) {
         }
 
         float best;
-        int hit = Scan::scan(a, pos, dir, best, n_tests, n_rescan);
+        int hit = Scan::scan(a, s_img, pos, dir, best, n_tests, n_rescan);
         n_scan++;
         if (best == INFINITY) { /* photonmap.cl:208-209 */
             alive = false;
@@ -153,19 +290,18 @@ __global__ __launch_bounds__(256) void k_bake(BakeArgs a) {
                                            mkf3(h.hnx, h.hny, h.hnz), h.hl, h.W, h.H, pos);
         if ((double)pos.z > 0.0005 || rng_next(rng) > 0.75f) {
             dir = sample_dir(rng, hn, mkf3(h.bux, h.buy, h.buz), mkf3(h.bvx, h.bvy, h.bvz), false);
-            if (pos.z < 1e-5f) {
+            const bool floor = pos.z < 1e-5f;
+            if (floor) {
                 col.y *= 0.85f;
                 col.z *= 0.7f;
             }
             col = mul3(col, 0.9f);
+            sid = (sid & 512) | ((sid & 511) << 1) | (floor ? 1 : 0);
         } else {
             float two = 2.0f * dot3(hn, dir);
             dir = sub3(dir, mul3(hn, two));
         }
-        unsigned long long *t = a.lm + 4 * (size_t)texel;
-        atomicAdd(t + 0, fx(col.x));
-        atomicAdd(t + 1, fx(col.y));
-        atomicAdd(t + 2, fx(col.z));
+        Acc::deposit(a, texel, sid, col);
         n_dep++;
         if (TRACE) {
             EventDev e;
@@ -196,6 +332,31 @@ __global__ __launch_bounds__(256) void k_bake(BakeArgs a) {
     }
 }
 
+/* AccState -> int64 fixed point: lm[t][c] += sum_s counts[s][t] * colour_fx[s][c]; counts zeroed.
+   One thread per texel; each read of counts[s][*] is coalesced across the block. */
+__global__ __launch_bounds__(256) void k_reduce_states(unsigned int *__restrict__ counts,
+                                                       const long long *__restrict__ colfx,
+                                                       unsigned long long *__restrict__ lm, int n) {
+    const int t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (t >= n) return;
+    long long r = 0, g = 0, b = 0;
+    cptr<long long> C = (cptr<long long>)colfx;
+    for (int s = 0; s < FMGI_COLOUR_STATES; s++) {
+        unsigned int *p = counts + (size_t)s * n + t;
+        const unsigned int k = *p;
+        if (k) {
+            r += (long long)k * C[3 * s + 0];
+            g += (long long)k * C[3 * s + 1];
+            b += (long long)k * C[3 * s + 2];
+            *p = 0;
+        }
+    }
+    unsigned long long *q = lm + 4 * (size_t)t;
+    q[0] += (unsigned long long)r;
+    q[1] += (unsigned long long)g;
+    q[2] += (unsigned long long)b;
+}
+
 __global__ void k_finalize(const unsigned long long *__restrict__ lm, const float4 *__restrict__ tin,
                            float4 *__restrict__ tout, int64_t n) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
@@ -219,17 +380,34 @@ __global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, flo
     c[i] = b;
 }
 
+template <class Scan, class Acc>
+void launch3(const BakeArgs &a, bool trace, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+    if (trace)
+        hipLaunchKernelGGL((k_bake<Scan, Acc, true>), grid, block, lds, s, a);
+    else
+        hipLaunchKernelGGL((k_bake<Scan, Acc, false>), grid, block, lds, s, a);
+}
+
 } // namespace
 
-int fmgi_block_size() { return 256; }
+hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, bool trace, int grid_blocks, int block, hipStream_t s) {
+    dim3 grid(grid_blocks), blk(block);
+    const bool st = a.counts != nullptr;
+    if (kernel == 1) { /* FMGI_KERNEL_FAST */
+        const size_t lds = (size_t)a.fimg_bytes;
+        if (st) launch3<ScanFast, AccState>(a, trace, grid, blk, lds, s);
+        else launch3<ScanFast, AccFx3>(a, trace, grid, blk, lds, s);
+    } else {
+        if (st) launch3<ScanExact, AccState>(a, trace, grid, blk, 0, s);
+        else launch3<ScanExact, AccFx3>(a, trace, grid, blk, 0, s);
+    }
+    return hipGetLastError();
+}
 
-hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, bool trace, int grid_blocks, hipStream_t s) {
-    (void)kernel;
-    dim3 grid(grid_blocks), block(256);
-    if (trace)
-        hipLaunchKernelGGL((k_bake<ScanExact, true>), grid, block, 0, s, a);
-    else
-        hipLaunchKernelGGL((k_bake<ScanExact, false>), grid, block, 0, s, a);
+hipError_t fmgi_launch_reduce_states(unsigned int *counts, const long long *colfx, unsigned long long *lm, int n,
+                                     hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_reduce_states, dim3((n + 255) / 256), dim3(256), 0, s, counts, colfx, lm, n);
     return hipGetLastError();
 }
 

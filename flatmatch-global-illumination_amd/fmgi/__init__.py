@@ -18,7 +18,8 @@ import ctypes as C
 import numpy as np
 
 from . import scene
-from ._lib import KERNEL_EXACT, KERNEL_FAST, FmgiError, Geometry, Stats, check, load
+from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_STATE, KERNEL_EXACT, KERNEL_FAST, FmgiError, Geometry, Stats,
+                   check, load)
 from .scene import RECT_DTYPE, Scene
 
 LAUNCH_DTYPE = np.dtype(
@@ -41,6 +42,9 @@ __all__ = [
     "FmgiError",
     "KERNEL_EXACT",
     "KERNEL_FAST",
+    "ACCUM_AUTO",
+    "ACCUM_FX3",
+    "ACCUM_STATE",
     "LAUNCH_DTYPE",
     "EVENT_DTYPE",
     "device_count",
@@ -110,6 +114,15 @@ class Context:
         )
         self.scene = sc
 
+    def set_accumulation(self, mode: int):
+        """ACCUM_FX3 (3 int64 atomics per deposit), ACCUM_STATE (1 u32 counter per colour state and
+        texel) or ACCUM_AUTO. Both modes give identical bits."""
+        check(self.lib.fmgi_set_accumulation(self.h, mode), "fmgi_set_accumulation")
+
+    @property
+    def accumulation(self) -> int:
+        return int(self.lib.fmgi_get_accumulation(self.h))
+
     def plan(self, spa: int, wg: int = 256, rng_offsets=None) -> int:
         """Reference launch schedule. rng_offsets=None consumes libc rand() like the reference."""
         tot = C.c_uint64()
@@ -128,6 +141,8 @@ class Context:
         return out
 
     def bake_items(self, begin: int, end: int, lm_fx_ptr: int, kernel: int = KERNEL_FAST, stream: int = 0):
+        """Launch on `stream` (a hipStream_t as int; pass the stream that produced lm_fx). 0/None selects
+        the context's internal stream, which is NOT ordered with torch's default stream."""
         check(self.lib.fmgi_bake_items(self.h, begin, end, C.c_void_p(lm_fx_ptr), kernel, C.c_void_p(stream or None)),
               "fmgi_bake_items")
 

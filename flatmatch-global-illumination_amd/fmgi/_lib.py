@@ -19,6 +19,8 @@ EXPORTS = (
     "fmgi_create",
     "fmgi_destroy",
     "fmgi_set_scene",
+    "fmgi_set_accumulation",
+    "fmgi_get_accumulation",
     "fmgi_plan",
     "fmgi_get_plan",
     "fmgi_plan_count",
@@ -33,6 +35,9 @@ EXPORTS = (
 
 KERNEL_EXACT = 0
 KERNEL_FAST = 1
+ACCUM_AUTO = 0
+ACCUM_FX3 = 1
+ACCUM_STATE = 2
 
 
 class FmgiError(RuntimeError):
@@ -96,6 +101,8 @@ def load() -> C.CDLL:
         "fmgi_create": (vp, [C.c_int]),
         "fmgi_destroy": (None, [vp]),
         "fmgi_set_scene": (C.c_int, [vp, vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int]),
+        "fmgi_set_accumulation": (C.c_int, [vp, C.c_int]),
+        "fmgi_get_accumulation": (C.c_int, [vp]),
         "fmgi_plan": (i64, [vp, C.c_int, C.c_int, vp, i64, C.POINTER(u64)]),
         "fmgi_get_plan": (i64, [vp, vp, i64]),
         "fmgi_plan_count": (i64, [vp, C.c_int, vp, C.c_int, C.c_int, C.c_int, C.POINTER(u64)]),

@@ -73,6 +73,12 @@ enum {
 };
 
 enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1 };
+/* Deposit accumulation (both exact and order-free; results are identical):
+   FX3   three int64 fixed-point atomics per deposit into the lightmap;
+   STATE one u32 atomic per deposit into counts[colour state][texel] (4 KiB per texel of device memory),
+         folded into the int64 lightmap after every <= 5e8-photon chunk;
+   AUTO  STATE when the counters fit a 4 GiB budget, else FX3. */
+enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2 };
 
 /* Per-bake counters, accumulated on the device (one atomic per wave). */
 typedef struct fmgi_stats {
@@ -119,6 +125,11 @@ void fmgi_destroy(fmgi_context *ctx);
    exactly as photonmap.cl would compute them. */
 int fmgi_set_scene(fmgi_context *ctx, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
                    int num_windows, const fmgi_rect *lights, int num_lights, int num_texels);
+
+/* Select the accumulation mode (FMGI_ACCUM_*); takes effect for the current and later scenes. */
+int fmgi_set_accumulation(fmgi_context *ctx, int mode);
+/* The mode in effect (FMGI_ACCUM_FX3 or FMGI_ACCUM_STATE). */
+int fmgi_get_accumulation(fmgi_context *ctx);
 
 /* Reference launch schedule for spa / wg. If rng_offsets is NULL, libc rand() is called once per
    launch in reference order; otherwise offsets are taken from rng_offsets[0..n_offsets).

@@ -29,7 +29,12 @@ fi
 
 CLFLAGS="-x cl -cl-std=CL1.2 -Xclang -finclude-default-header -target amdgcn-amd-amdhsa -mcpu=gfx950 -O3"
 $CLANG $CLFLAGS -Wno-nan-infinity-disabled -cl-fp32-correctly-rounded-divide-sqrt -ffp-contract=off "$REF/photonmap.cl" -o "$OUT/photonmap_strict.hsaco"
+# The reference's own flag (-cl-fast-relaxed-math) implies finite-math-only, under which ROCm's clang
+# folds photonmap.cl:208 `dist_out == INFINITY` away: an escaping photon then dereferences hitObj == 0
+# and the kernel faults (observed on MI355X, gpurun_out/s1/ref.log). It is built for inspection only and
+# must not be launched; "relaxed" keeps every other fast-math relaxation and stays well defined.
 $CLANG $CLFLAGS -Wno-nan-infinity-disabled -cl-fast-relaxed-math "$REF/photonmap.cl" -o "$OUT/photonmap_fast.hsaco"
+$CLANG $CLFLAGS -Wno-nan-infinity-disabled -cl-unsafe-math-optimizations "$REF/photonmap.cl" -o "$OUT/photonmap_relaxed.hsaco"
 
 # Host C objects of the reference (flags as in the reference Makefile:21,26 minus -flto/-g).
 PNG_INC=${PNG_INC:-/opt/conda/include}

@@ -166,7 +166,10 @@ def ref_kernel_available(variant: str = "strict") -> bool:
 
 def ref_run_items(scene, source: int, is_window: int, rng_states, variant: str = "strict") -> np.ndarray:
     """Run the reference photonmap kernel (photonmap.cl:269) once per work item, each on a zeroed
-    lightColors buffer; returns float32 [n, numTexels, 4]."""
+    lightColors buffer; returns float32 [n, numTexels, 4]. Variant "fast" is refused: built with the
+    reference's -cl-fast-relaxed-math it faults on the first escaping photon (see build_ref.sh)."""
+    if variant not in ("strict", "relaxed"):
+        raise ValueError(f"reference variant {variant!r} is not launchable")
     global _ref
     if _ref is None:
         _ref = C.CDLL(os.path.join(HERE, "libref_runner.so"))

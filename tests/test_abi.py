@@ -53,7 +53,7 @@ def test_no_symbol_clashes_with_reference_objects():
                 "getDiffuseSkyRandomRay", "createBase", "add", "sub", "mul"}
     exported = _exports()
     assert not (exported & clashing)
-    extra = {s for s in exported if not s.startswith(("fmgi_", "__hip_cuid"))}
+    extra = {s for s in exported if not s.startswith("fmgi_")}
     assert extra == {"performGlobalIlluminationCl", "getGlobalIlluminationCl"}
 
 

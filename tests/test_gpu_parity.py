@@ -34,8 +34,9 @@ def offsets():
     return np.load(os.path.join(GOLDEN, "glibc_rand_4096.npy"))
 
 
-def _ctx(sc, spa, offsets):
+def _ctx(sc, spa, offsets, accum=fmgi.ACCUM_AUTO):
     ctx = fmgi.Context(0)
+    ctx.set_accumulation(accum)
     ctx.set_scene(sc)
     ctx.plan(spa, rng_offsets=offsets)
     return ctx
@@ -46,10 +47,11 @@ def _oracle_plan(sc, spa, offsets):
 
 
 def _bake_gpu(torch, ctx, b, e, kernel):
-    lm = torch.zeros((ctx.scene.num_texels, 4), dtype=torch.int64, device="cuda")
-    s = torch.cuda.current_stream()
-    ctx.bake_items(b, e, lm.data_ptr(), kernel, s.cuda_stream)
-    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):  # zero-fill and bake ordered on one (non-default) stream
+        lm = torch.zeros((ctx.scene.num_texels, 4), dtype=torch.int64, device="cuda")
+        ctx.bake_items(b, e, lm.data_ptr(), kernel, s.cuda_stream)
+    s.synchronize()
     return lm.cpu().numpy()
 
 
@@ -109,12 +111,17 @@ def test_per_photon_traces_boxes(torch_cuda, box200, box2000, offsets, kernel):
         ctx.close()
 
 
+ACCUMS = [fmgi.ACCUM_FX3, fmgi.ACCUM_STATE]
+
+
+@pytest.mark.parametrize("accum", ACCUMS)
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_lightmap_config1_exact(torch_cuda, example_scene, offsets, kernel):
+def test_lightmap_config1_exact(torch_cuda, example_scene, offsets, kernel, accum):
     """BASELINE config 1 (example.png, 1.1e6 photons): GPU int64 lightmap == oracle, bit for bit."""
     spa = 65_000
     L = _oracle_plan(example_scene, spa, offsets)
-    ctx = _ctx(example_scene, spa, offsets)
+    ctx = _ctx(example_scene, spa, offsets, accum)
+    assert ctx.accumulation == accum
     ctx.reset_stats()
     lm = _bake_gpu(torch_cuda, ctx, 0, ctx.total_items, kernel)
     olm, ost = O.bake(example_scene, L)
@@ -126,12 +133,13 @@ def test_lightmap_config1_exact(torch_cuda, example_scene, offsets, kernel):
     ctx.close()
 
 
+@pytest.mark.parametrize("accum", ACCUMS)
 @pytest.mark.parametrize("kernel", KERNELS)
-def test_lightmap_box_prefix_exact(torch_cuda, box200, box2000, offsets, kernel):
+def test_lightmap_box_prefix_exact(torch_cuda, box200, box2000, offsets, kernel, accum):
     for sc, items in ((box200, 20_000), (box2000, 1_000)):
         spa = 172_413_793
         L = _oracle_plan(sc, spa, offsets)
-        ctx = _ctx(sc, spa, offsets)
+        ctx = _ctx(sc, spa, offsets, accum)
         lm = _bake_gpu(torch_cuda, ctx, 5_000, 5_000 + items, kernel)
         olm, _ = O.bake(sc, L, 5_000, 5_000 + items)
         assert np.array_equal(lm[:, :3], olm)
@@ -142,14 +150,15 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     """Config 3 sized work (a 1e8-photon slice): order-free exact accumulation means any split of the
     item range, and any repetition, gives identical bits."""
     spa = 172_413_793
-    ctx = _ctx(box200, spa, offsets)
-    n = 1_000_000  # 1e8 photons
+    ctx = _ctx(box200, spa, offsets, fmgi.ACCUM_STATE)
+    n = 12_000_000  # 1.2e9 photons: crosses the 5e6-item AccState chunk boundary twice
     a = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
-    b1 = _bake_gpu(torch_cuda, ctx, 0, 333_333, fmgi.KERNEL_FAST)
-    b2 = _bake_gpu(torch_cuda, ctx, 333_333, n, fmgi.KERNEL_FAST)
+    b1 = _bake_gpu(torch_cuda, ctx, 0, 3_333_333, fmgi.KERNEL_FAST)
+    b2 = _bake_gpu(torch_cuda, ctx, 3_333_333, n, fmgi.KERNEL_FAST)
+    ctx.set_accumulation(fmgi.ACCUM_FX3)
     c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
     assert np.array_equal(a, b1 + b2)
-    assert np.array_equal(a, c)
+    assert np.array_equal(a, c)  # the two accumulation modes agree bit for bit
     ctx.reset_stats()
     _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
     st = ctx.stats()
@@ -170,11 +179,13 @@ def test_finalize_matches_oracle(torch_cuda, example_scene, offsets):
     torch = torch_cuda
     lm = torch.zeros((example_scene.num_texels, 4), dtype=torch.int64)
     lm[:, :3] = torch.from_numpy(olm)
-    lm = lm.cuda()
-    t_in = torch.from_numpy(tin).cuda()
-    t_out = torch.empty_like(t_in)
-    ctx.finalize(lm.data_ptr(), t_in.data_ptr(), t_out.data_ptr(), torch.cuda.current_stream().cuda_stream)
-    torch.cuda.synchronize()
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        lm = lm.cuda()
+        t_in = torch.from_numpy(tin).cuda()
+        t_out = torch.empty_like(t_in)
+        ctx.finalize(lm.data_ptr(), t_in.data_ptr(), t_out.data_ptr(), s.cuda_stream)
+    s.synchronize()
     assert np.array_equal(t_out.cpu().numpy().view(np.uint32), O.finalize(olm, tin).view(np.uint32))
     ctx.close()
 
@@ -210,7 +221,7 @@ def test_reference_kernel_pins_oracle(torch_cuda, example_scene, offsets):
     spa = 65_000
     L = _oracle_plan(example_scene, spa, offsets)
     states = [(g + int(L[0]["rng_offset"])) & 0xFFFFFFFF for g in range(32)]
-    ref = O.ref_run_items(example_scene, 0, 1, states, "strict")
+    ref = O.ref_run_items(example_scene, 0, 1, states, "strict")  # never "fast": it faults (build_ref.sh)
     same = 0
     for k, st in enumerate(states):
         mine = O.trace_item_f32(example_scene, 0, 1, st)

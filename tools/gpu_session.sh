@@ -1,5 +1,11 @@
 #!/usr/bin/env bash
-# One gpurun session: GPU tests -> reference-kernel pin -> bench -> rocprofv3 kernel-trace summary.
+# One gpurun session. Steps (FMGI_STEPS, space separated):
+#   tests            pytest -m gpu
+#   ref              reference-kernel pin (tests/golden/make_ref_fixtures.py)
+#   bench            python bench.py $BENCH_ARGS
+#   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
+#   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
+#   pmc              rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on a short bench ($PROF_ARGS)
 # Each GPU step has its own time limit; a crash/timeout (rc > 1) stops the session.
 set -u
 cd "$(dirname "$0")/.."
@@ -7,19 +13,23 @@ OUT=gpurun_out/${FMGI_SESSION:-s1}
 mkdir -p "$OUT"
 step() {  # step <name> <timeout-seconds> <cmd...>
     local name=$1 t=$2; shift 2
-    echo "== $name"; date +%T
+    echo "== $name ($(date +%T))"
     timeout -k 10 "$t" "$@" > "$OUT/$name.log" 2>&1
     local rc=$?
-    echo "   rc=$rc"; tail -n 5 "$OUT/$name.log"
+    echo "   rc=$rc"; tail -n 3 "$OUT/$name.log" | cut -c1-2000
     if [ $rc -gt 1 ]; then echo "stopping after $name (rc=$rc)"; exit $rc; fi
 }
 python -c "import __graft_entry__ as g; g.build()" || exit 3
+export TMPDIR=/tmp
 for s in ${FMGI_STEPS:-tests ref bench prof}; do
   case $s in
     tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
-    prof)  export TMPDIR=/tmp; step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${BENCH_ARGS:-} ;;
+    bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; step "$s" 600 python bench.py ${!v:-} ;;
+    prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
+           step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
   esac
 done
 echo "session done"
