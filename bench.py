@@ -92,7 +92,8 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
-    ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state"])
+    ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state", "none"],
+                    help="none = PROFILING ONLY (deposits discarded; lightmap wrong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     args = ap.parse_args()
@@ -101,6 +102,7 @@ def main():
     import torch.distributed as dist
 
     import fmgi
+    from fmgi import parallel
 
     rank = int(os.environ.get("RANK", "0"))
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -118,13 +120,13 @@ def main():
     kernel = fmgi.KERNEL_FAST if args.kernel == "fast" else fmgi.KERNEL_EXACT
 
     ctx = fmgi.Context(local)
-    ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE}[args.accum])
+    ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE,
+                          "none": fmgi.ACCUM_NONE}[args.accum])
     ctx.set_scene(sc)
     libc = ctypes.CDLL(None)
     libc.srand(1)  # the unseeded state main.c runs with; every rank builds the same schedule
     total_items = ctx.plan(spa)  # consumes rand() once per reference launch
-    b = total_items * rank // world
-    e = total_items * (rank + 1) // world
+    b, e = parallel.shard_range(total_items, rank, world)
     photons_per_step = 100 * total_items
 
     dev = torch.device("cuda", local)
@@ -149,7 +151,7 @@ def main():
             e_ev.record(stream)
             k_ms.append((s_ev, e_ev))
         if world > 1:
-            dist.reduce(lm, dst=0)
+            parallel.reduce_lightmap(lm, dst=0)  # RCCL over xGMI
         if rank == 0:
             ctx.finalize(lm.data_ptr(), tex_in.data_ptr(), tex_out.data_ptr(), sptr)
 
@@ -213,7 +215,7 @@ def main():
                 "spa": spa,
                 "photons_per_step": photons_per_step,
                 "kernel": args.kernel,
-                "accumulation": {1: "fx3", 2: "state"}[ctx.accumulation],
+                "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)"}[ctx.accumulation],
                 "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
             },
             "roofline": {

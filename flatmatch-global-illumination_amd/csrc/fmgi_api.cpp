@@ -243,7 +243,7 @@ struct fmgi_context {
     /* accumulation: FMGI_ACCUM_FX3 or FMGI_ACCUM_STATE (counts[1024][numTexels] + colour table) */
     int accum_req = FMGI_ACCUM_AUTO;
     int accum = FMGI_ACCUM_FX3;
-    unsigned int *d_counts = nullptr;
+    unsigned long long *d_counts = nullptr;
     long long *d_colfx = nullptr;
 };
 
@@ -316,16 +316,16 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     delete c;
 }
 
-/* AccState needs 4 KiB of counters per texel; above this budget (or on request) AccFx3 is used. */
-static const size_t kStateBudget = (size_t)4 << 30;
+/* AccState needs 8 KiB of u64 counters per texel; above this budget (or on request) AccFx3 is used. */
+static const size_t kStateBudget = (size_t)8 << 30;
 
 static int configure_accum(fmgi_context *c) {
-    size_t bytes = (size_t)FMGI_COLOUR_STATES * (size_t)c->num_texels * sizeof(unsigned int);
+    size_t bytes = (size_t)FMGI_COLOUR_STATES * (size_t)c->num_texels * sizeof(unsigned long long);
     int want = c->accum_req;
     if (want == FMGI_ACCUM_AUTO) want = (bytes && bytes <= kStateBudget) ? FMGI_ACCUM_STATE : FMGI_ACCUM_FX3;
     hipFree(c->d_counts);
     c->d_counts = nullptr;
-    c->accum = FMGI_ACCUM_FX3;
+    c->accum = want == FMGI_ACCUM_NONE ? FMGI_ACCUM_NONE : FMGI_ACCUM_FX3;
     if (want != FMGI_ACCUM_STATE || !bytes) return FMGI_OK;
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipMalloc(&c->d_counts, bytes));
@@ -340,7 +340,7 @@ static int configure_accum(fmgi_context *c) {
 }
 
 FMGI_API int fmgi_set_accumulation(fmgi_context *c, int mode) {
-    if (!c || mode < FMGI_ACCUM_AUTO || mode > FMGI_ACCUM_STATE) return set_err(FMGI_ERR_ARG, "bad accumulation mode");
+    if (!c || mode < FMGI_ACCUM_AUTO || mode > FMGI_ACCUM_NONE) return set_err(FMGI_ERR_ARG, "bad accumulation mode");
     c->accum_req = mode;
     if (c->device == FMGI_HOST_ONLY || c->num_texels == 0) return FMGI_OK;
     return configure_accum(c);
@@ -479,11 +479,15 @@ FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
     return n;
 }
 
-static int grid_blocks(const fmgi_context *c, uint64_t items) {
-    /* persistent grid: 8 blocks of 256 lanes per CU (32 waves/CU); never more lanes than items */
-    uint64_t lanes_max = (uint64_t)c->num_cus * 8 * 256;
+static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, uint64_t items) {
+    /* persistent grid: exactly the blocks that are resident at once (occupancy from the VGPR/SGPR/LDS
+       use of the kernel actually launched), so no block starts late and lengthens the tail; never more
+       lanes than work items */
+    int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, c->fimg_bytes);
+    if (per_cu <= 0) per_cu = 4;
+    uint64_t lanes_max = (uint64_t)c->num_cus * per_cu * block;
     uint64_t lanes = std::min<uint64_t>(items, lanes_max);
-    return (int)std::max<uint64_t>(1, (lanes + 255) / 256);
+    return (int)std::max<uint64_t>(1, (lanes + block - 1) / block);
 }
 
 static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
@@ -518,18 +522,12 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.events = events;
     a.ev_counts = counts;
     a.rng_final = rngf;
-    /* AccState: u32 counters must not overflow -> at most 5e6 work items (5e8 photons, <= 4e9
-       deposits) per chunk, each chunk folded into the int64 lightmap (and the counters re-zeroed) */
-    const uint64_t chunk = a.counts ? (uint64_t)5000000 : (e - b);
-    for (uint64_t cb = b; cb < e; cb += chunk) {
-        const uint64_t ce = std::min(e, cb + chunk);
-        a.item_begin = cb;
-        a.item_end = ce;
-        HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
-        HIPCHK(fmgi_launch_bake(a, kernel, trace, grid_blocks(c, ce - cb), 256, s));
-        if (a.counts)
-            HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
-    }
+    const int block = 256;
+    HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
+    HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid_blocks(c, kernel, c->accum, trace, block, e - b), block, s));
+    /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
+    if (a.counts)
+        HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
     return FMGI_OK;
 }
 

@@ -38,8 +38,8 @@ struct BakeArgs {
     int fJ[3];
     const int32_t *general;
     int ngeneral;
-    /* AccState accumulation: u32 counts[FMGI_COLOUR_STATES][num_texels] (NULL -> AccFx3) */
-    unsigned int *counts;
+    /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
+    unsigned long long *counts;
     int num_texels;
     /* debug trace (TRACE kernels only) */
     void *events;                  /* fmgi_event[(item - item_begin) * 800 + k]                     */
@@ -51,9 +51,12 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 
 #define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
 
-hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, bool trace, int grid_blocks, int block, hipStream_t s);
-hipError_t fmgi_launch_reduce_states(unsigned int *counts, const long long *colfx, unsigned long long *lm, int n,
-                                     hipStream_t s);
+/* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only) */
+hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
+                            hipStream_t s);
+int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);
+hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long *colfx, unsigned long long *lm,
+                                     int n, hipStream_t s);
 hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, float *tout, int64_t n,
                                 hipStream_t s);
 hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, hipStream_t s);

@@ -209,12 +209,18 @@ struct AccFx3 {
     }
 };
 
-/* one u32 count per (colour state, texel): the deposited colour is a function of the state
+/* one u64 count per (colour state, texel): the deposited colour is a function of the state
    (source kind + the floor/non-floor sequence of diffuse bounces, see k_reduce_states) */
 struct AccState {
     static __device__ __forceinline__ void deposit(const BakeArgs &a, int texel, int sid, f3) {
-        atomicAdd(a.counts + (size_t)sid * a.num_texels + texel, 1u);
+        atomicAdd(a.counts + (size_t)sid * a.num_texels + texel, 1ull);
     }
+};
+
+/* PROFILING ONLY (FMGI_ACCUM_NONE): deposits are discarded, so a bake measures the tracing work alone.
+   The lightmap stays zero; never used for results. */
+struct AccNone {
+    static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
 };
 
 /* ---- the per-lane photon state machine ------------------------------------------------------- */
@@ -334,7 +340,7 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
 
 /* AccState -> int64 fixed point: lm[t][c] += sum_s counts[s][t] * colour_fx[s][c]; counts zeroed.
    One thread per texel; each read of counts[s][*] is coalesced across the block. */
-__global__ __launch_bounds__(256) void k_reduce_states(unsigned int *__restrict__ counts,
+__global__ __launch_bounds__(256) void k_reduce_states(unsigned long long *__restrict__ counts,
                                                        const long long *__restrict__ colfx,
                                                        unsigned long long *__restrict__ lm, int n) {
     const int t = blockIdx.x * blockDim.x + threadIdx.x;
@@ -342,8 +348,8 @@ __global__ __launch_bounds__(256) void k_reduce_states(unsigned int *__restrict_
     long long r = 0, g = 0, b = 0;
     cptr<long long> C = (cptr<long long>)colfx;
     for (int s = 0; s < FMGI_COLOUR_STATES; s++) {
-        unsigned int *p = counts + (size_t)s * n + t;
-        const unsigned int k = *p;
+        unsigned long long *p = counts + (size_t)s * n + t;
+        const unsigned long long k = *p;
         if (k) {
             r += (long long)k * C[3 * s + 0];
             g += (long long)k * C[3 * s + 1];
@@ -388,23 +394,49 @@ void launch3(const BakeArgs &a, bool trace, dim3 grid, dim3 block, size_t lds, h
         hipLaunchKernelGGL((k_bake<Scan, Acc, false>), grid, block, lds, s, a);
 }
 
+template <class Scan, class Acc>
+const void *kernel_ptr(bool trace) {
+    return trace ? (const void *)&k_bake<Scan, Acc, true> : (const void *)&k_bake<Scan, Acc, false>;
+}
+
+const void *bake_kernel(int kernel, int accum, bool trace) {
+    if (kernel == 1) {
+        if (accum == 2) return kernel_ptr<ScanFast, AccState>(trace);
+        if (accum == 3) return kernel_ptr<ScanFast, AccNone>(trace);
+        return kernel_ptr<ScanFast, AccFx3>(trace);
+    }
+    if (accum == 2) return kernel_ptr<ScanExact, AccState>(trace);
+    if (accum == 3) return kernel_ptr<ScanExact, AccNone>(trace);
+    return kernel_ptr<ScanExact, AccFx3>(trace);
+}
+
 } // namespace
 
-hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, bool trace, int grid_blocks, int block, hipStream_t s) {
+int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes) {
+    int n = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bake_kernel(kernel, accum, trace), block,
+                                                     kernel == 1 ? (size_t)lds_bytes : 0) != hipSuccess)
+        return 0;
+    return n;
+}
+
+hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
+                            hipStream_t s) {
     dim3 grid(grid_blocks), blk(block);
-    const bool st = a.counts != nullptr;
+    const size_t lds = kernel == 1 ? (size_t)a.fimg_bytes : 0;
     if (kernel == 1) { /* FMGI_KERNEL_FAST */
-        const size_t lds = (size_t)a.fimg_bytes;
-        if (st) launch3<ScanFast, AccState>(a, trace, grid, blk, lds, s);
+        if (accum == 2) launch3<ScanFast, AccState>(a, trace, grid, blk, lds, s);
+        else if (accum == 3) launch3<ScanFast, AccNone>(a, trace, grid, blk, lds, s);
         else launch3<ScanFast, AccFx3>(a, trace, grid, blk, lds, s);
     } else {
-        if (st) launch3<ScanExact, AccState>(a, trace, grid, blk, 0, s);
-        else launch3<ScanExact, AccFx3>(a, trace, grid, blk, 0, s);
+        if (accum == 2) launch3<ScanExact, AccState>(a, trace, grid, blk, lds, s);
+        else if (accum == 3) launch3<ScanExact, AccNone>(a, trace, grid, blk, lds, s);
+        else launch3<ScanExact, AccFx3>(a, trace, grid, blk, lds, s);
     }
     return hipGetLastError();
 }
 
-hipError_t fmgi_launch_reduce_states(unsigned int *counts, const long long *colfx, unsigned long long *lm, int n,
+hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long *colfx, unsigned long long *lm, int n,
                                      hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_reduce_states, dim3((n + 255) / 256), dim3(256), 0, s, counts, colfx, lm, n);

@@ -38,6 +38,7 @@ KERNEL_FAST = 1
 ACCUM_AUTO = 0
 ACCUM_FX3 = 1
 ACCUM_STATE = 2
+ACCUM_NONE = 3  # profiling only: deposits discarded
 
 
 class FmgiError(RuntimeError):

@@ -1,0 +1,27 @@
+"""Photon-batch data parallelism across GPUs (one process per GPU, torch.distributed).
+
+The reference has a single OpenCL device (global_illumination_cl.c:279-281). Its launch schedule
+flattens into independent work items (gid + rng_offset fully determines a work item's photons,
+photonmap.cl:272), so ranks take contiguous, equal shards of the flattened item list -- no data-path
+communication -- and the only exchange is one sum-reduce of the per-rank int64 fixed-point lightmaps
+(RCCL over xGMI on MI355X nodes, gloo on CPU). Integer addition is associative, so the reduced
+lightmap is bit-identical for any world size and any shard split.
+"""
+from __future__ import annotations
+
+
+def shard_range(total_items: int, rank: int, world: int) -> tuple[int, int]:
+    """Contiguous shard [begin, end) of the flattened work-item list for `rank` of `world`
+    (sizes differ by at most one item)."""
+    if world <= 0 or not 0 <= rank < world:
+        raise ValueError(f"bad rank {rank} of world {world}")
+    return total_items * rank // world, total_items * (rank + 1) // world
+
+
+def reduce_lightmap(lm, dst: int = 0, group=None):
+    """Sum the int64 [numTexels, 4] lightmaps of all ranks into rank `dst` (in place there)."""
+    import torch.distributed as dist
+
+    if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
+        dist.reduce(lm, dst=dst, op=dist.ReduceOp.SUM, group=group)
+    return lm

@@ -75,10 +75,11 @@ enum {
 enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1 };
 /* Deposit accumulation (both exact and order-free; results are identical):
    FX3   three int64 fixed-point atomics per deposit into the lightmap;
-   STATE one u32 atomic per deposit into counts[colour state][texel] (4 KiB per texel of device memory),
-         folded into the int64 lightmap after every <= 5e8-photon chunk;
-   AUTO  STATE when the counters fit a 4 GiB budget, else FX3. */
-enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2 };
+   STATE one u64 atomic per deposit into counts[colour state][texel] (8 KiB per texel of device memory),
+         folded into the int64 lightmap at the end of every fmgi_bake_items;
+   AUTO  STATE when the counters fit an 8 GiB budget, else FX3;
+   NONE  PROFILING ONLY: deposits are discarded (measures the tracing work alone; wrong lightmap). */
+enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2, FMGI_ACCUM_NONE = 3 };
 
 /* Per-bake counters, accumulated on the device (one atomic per wave). */
 typedef struct fmgi_stats {

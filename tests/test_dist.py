@@ -1,0 +1,74 @@
+"""Multi-rank path on CPU: world_size 2 with the gloo backend.
+
+Each rank bakes its shard (fmgi.parallel.shard_range) -- here with the oracle standing in for the GPU,
+since this container has none -- and the int64 lightmaps are summed with fmgi.parallel.reduce_lightmap
+(the same call bench.py makes over RCCL). The reduced lightmap must equal the single-process bake bit
+for bit, for several shard counts."""
+import os
+import socket
+
+import numpy as np
+import pytest
+import torch
+import torch.distributed as dist
+import torch.multiprocessing as mp
+
+from conftest import GOLDEN, ORACLE, PKG
+
+
+def _free_port():
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _worker(rank, world, port, items, out_path):
+    import sys
+
+    sys.path[:0] = [PKG, ORACLE]
+    import fm_oracle as O
+    from fmgi import parallel, scene
+
+    os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port))
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    sc = scene.box_scene(200)
+    offs = np.load(os.path.join(GOLDEN, "glibc_rand_4096.npy"))
+    L = O.schedule_with_offsets(sc, 172_413_793, offs)
+    b, e = parallel.shard_range(items, rank, world)
+    lm3, _ = O.bake(sc, L, b, e, nthreads=2)
+    lm = torch.zeros((sc.num_texels, 4), dtype=torch.int64)
+    lm[:, :3] = torch.from_numpy(lm3)
+    parallel.reduce_lightmap(lm, dst=0)
+    if rank == 0:
+        np.save(out_path, lm.numpy())
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+@pytest.mark.parametrize("world", [2])
+def test_sharded_bake_reduces_to_single_process_result(world, tmp_path, box200):
+    import fm_oracle as O
+
+    items = 300
+    out = str(tmp_path / "lm.npy")
+    mp.spawn(_worker, args=(world, _free_port(), items, out), nprocs=world, join=True)
+    got = np.load(out)
+    offs = np.load(os.path.join(GOLDEN, "glibc_rand_4096.npy"))
+    L = O.schedule_with_offsets(box200, 172_413_793, offs)
+    exp, _ = O.bake(box200, L, 0, items)
+    assert np.array_equal(got[:, :3], exp)
+    assert not got[:, 3].any()
+
+
+def test_shard_ranges_tile_the_item_list():
+    from fmgi import parallel
+
+    for total in (0, 1, 7, 10_000_026, 100_000_256):
+        for world in (1, 2, 3, 4, 8):
+            rs = [parallel.shard_range(total, r, world) for r in range(world)]
+            assert rs[0][0] == 0 and rs[-1][1] == total
+            assert all(rs[i][1] == rs[i + 1][0] for i in range(world - 1))
+            sizes = [e - b for b, e in rs]
+            assert max(sizes) - min(sizes) <= 1
+    with pytest.raises(ValueError):
+        parallel.shard_range(10, 2, 2)

@@ -151,10 +151,10 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     item range, and any repetition, gives identical bits."""
     spa = 172_413_793
     ctx = _ctx(box200, spa, offsets, fmgi.ACCUM_STATE)
-    n = 12_000_000  # 1.2e9 photons: crosses the 5e6-item AccState chunk boundary twice
+    n = ctx.total_items  # BASELINE config 3 at full size: 1,000,012,800 photons
     a = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
-    b1 = _bake_gpu(torch_cuda, ctx, 0, 3_333_333, fmgi.KERNEL_FAST)
-    b2 = _bake_gpu(torch_cuda, ctx, 3_333_333, n, fmgi.KERNEL_FAST)
+    b1 = _bake_gpu(torch_cuda, ctx, 0, n // 3, fmgi.KERNEL_FAST)
+    b2 = _bake_gpu(torch_cuda, ctx, n // 3, n, fmgi.KERNEL_FAST)
     ctx.set_accumulation(fmgi.ACCUM_FX3)
     c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
     assert np.array_equal(a, b1 + b2)
