@@ -194,6 +194,15 @@ def main():
         ks = kernel_ms / 1e3
         achieved_tf = flops / ks / 1e12
         achieved_gbs = hbm_bytes / ks / 1e9
+        # memory-side atomic adds issued per second by the bake (1 per deposit for the colour-state
+        # counters, 3 for int64 RGB); ~20e9/s is the chip's rate for lane-scattered atomics
+        # (MI355X_MICROARCH.md §Global float atomics: ~0.08 TB/s of 4-B adds)
+        per_dep = {1: 3, 2: 1, 3: 0}[ctx.accumulation]
+        atomic_rate = per_dep * per_launch_deps / ks
+        atomics = {"per_deposit": per_dep, "achieved_per_s": atomic_rate, "ceiling_per_s": 2.0e10,
+                   "frac": atomic_rate / 2.0e10}
+        binding = ("memory-side atomic rate" if atomic_rate > 0.8 * 2.0e10 else
+                   "fp32 VALU (phase-1 filter + exact verification)")
         out = {
             "metric": METRIC,
             "value": value,
@@ -219,17 +228,24 @@ def main():
                 "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
             },
             "roofline": {
-                "bound": "mfma",
-                "pipe": "fp32 VALU (no MFMA instructions; gfx950's dense FP32 peak is the same 157.3 TF for VALU and MFMA)",
-                "achieved": achieved_tf,
-                "peak": FP32_PEAK_TFLOPS,
-                "unit": "TFLOP/s",
-                "frac": achieved_tf / FP32_PEAK_TFLOPS,
+                # BASELINE metric: achieved HBM GB/s of the dominant kernel (the bake), algorithmic bytes
+                # per SURVEY.md §8d (12 B per deposit + 16 B per texel written back) / HIP-event kernel time
+                "bound": "hbm",
+                "achieved": achieved_gbs,
+                "peak": HBM_PEAK_GBS,
+                "unit": "GB/s",
+                "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": pmc_traffic(args.config),
                 "kernel_ms": kernel_ms,
-                "algorithmic_flops_per_launch": flops,
-                "hbm": {"achieved": achieved_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                        "frac": achieved_gbs / HBM_PEAK_GBS, "algorithmic_bytes_per_launch": hbm_bytes},
+                "algorithmic_bytes_per_launch": hbm_bytes,
+                "binding": binding,
+                "atomics": atomics,
+                "compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
+                            "frac": achieved_tf / FP32_PEAK_TFLOPS,
+                            "algorithmic_flops_per_launch": flops,
+                            "note": "SURVEY.md §8d brute-force accounting (40 flops/rect test + 150/scan); the fast "
+                                    "scan does ~15 VALU ops per front-facing test, so frac > 1 measures the "
+                                    "algorithmic saving, not the hardware"},
             },
             "per_photon": {
                 "scans": scans / photons_done,
