@@ -251,6 +251,9 @@ def main():
                 "scans": scans / photons_done,
                 "deposits": deposits / photons_done,
                 "rect_tests_evaluated": st["tests"] / max(st["photons"], 1),
+                "exact_rescans_per_scan": st["exact_rescans"] / max(st["scans"], 1),
+                "rescans_tie_per_scan": st["rescans_tie"] / max(st["scans"], 1),
+                "rescans_invalid_per_scan": st["rescans_invalid"] / max(st["scans"], 1),
             },
         }
         if world == 1 and not args.no_cpu_baseline:

@@ -561,6 +561,8 @@ FMGI_API int fmgi_get_stats(fmgi_context *c, fmgi_stats *out) {
     out->escapes = v[KSTAT_ESCAPES];
     out->exact_rescans = v[KSTAT_RESCANS];
     out->tests = v[KSTAT_TESTS];
+    out->rescans_tie = v[KSTAT_TIES];
+    out->rescans_invalid = v[KSTAT_INVALID];
     return FMGI_OK;
 }
 
@@ -626,6 +628,15 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
 
 /* ---- the drop-in entry points ----------------------------------------------------------------- */
 
+/*
+ * One bake of a reference Geometry on all GPUs of the node (FMGI_GPUS, default: every visible device,
+ * at most 8). The reference launch schedule is built once (libc rand() consumed exactly as the
+ * reference does, global_illumination_cl.c:251) and its flattened work items are split into equal
+ * contiguous shards, one per GPU; each GPU accumulates its own exact int64 lightmap, and the shards are
+ * summed on GPU 0 over xGMI peer copies (integer sums: the result is bit-identical for any GPU count).
+ * FMGI_SHARDS (tests only) splits into more shards than GPUs, round-robin, to exercise the reduction on
+ * a single device.
+ */
 static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_out, bool verbose) {
     if (!geo) return set_err(FMGI_ERR_ARG, "null geometry");
     const char *wg_env = getenv("FMGI_WG");
@@ -635,43 +646,89 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     int kernel = (k_env && !strcmp(k_env, "exact")) ? FMGI_KERNEL_EXACT : FMGI_KERNEL_FAST;
     int ndev = fmgi_device_count();
     if (ndev <= 0) return set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
-    fmgi_context *c = fmgi_create(0);
-    if (!c) return FMGI_ERR_HIP;
-    int rc = fmgi_set_scene(c, geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
-                            geo->numLights, geo->numTexels);
+    const char *g_env = getenv("FMGI_GPUS");
+    int ngpu = g_env ? atoi(g_env) : std::min(ndev, 8);
+    ngpu = std::max(1, std::min(ngpu, ndev));
+    const char *s_env = getenv("FMGI_SHARDS");
+    int nshard = s_env ? std::max(1, std::min(atoi(s_env), 64)) : ngpu;
+
+    std::vector<fmgi_context *> ctx((size_t)nshard, nullptr);
+    std::vector<void *> lm((size_t)nshard, nullptr);
+    void *d_tex = nullptr, *d_stage = nullptr;
+    size_t tb = (size_t)geo->numTexels * 16;
     uint64_t items = 0;
-    if (rc == FMGI_OK) {
-        int64_t nl = fmgi_plan(c, spa, wg, nullptr, 0, &items);
+    int rc = FMGI_OK;
+    for (int k = 0; k < nshard && rc == FMGI_OK; k++) {
+        ctx[k] = fmgi_create(k % ngpu);
+        if (!ctx[k]) { rc = FMGI_ERR_HIP; break; }
+        rc = fmgi_set_scene(ctx[k], geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
+                            geo->numLights, geo->numTexels);
+        if (rc != FMGI_OK) break;
+        int64_t nl;
+        if (k == 0) {
+            nl = fmgi_plan(ctx[0], spa, wg, nullptr, 0, &items); /* the one rand() sequence */
+        } else {
+            std::vector<int32_t> offs;
+            for (const LaunchDev &L : ctx[0]->h_launches) offs.push_back(L.rng_offset);
+            nl = fmgi_plan(ctx[k], spa, wg, offs.data(), (int64_t)offs.size(), nullptr);
+        }
         if (nl < 0) rc = (int)nl;
-        else if (verbose) {
+        else if (k == 0 && verbose) {
             hipDeviceProp_t prop;
-            hipGetDeviceProperties(&prop, c->device);
-            printf("[INF] Selected device '%s'\n\n", prop.name);
+            if (hipGetDeviceProperties(&prop, 0) != hipSuccess) prop.name[0] = 0;
+            printf("[INF] Selected device '%s' (x%d)\n\n", prop.name, ngpu);
             printf("photon-mapping %d light sources with %llu M samples in %lld reference launches\n",
-                   c->nsrcs, (unsigned long long)(items * 100 / 1000000), (long long)nl);
+                   ctx[0]->nsrcs, (unsigned long long)(items * 100 / 1000000), (long long)nl);
             fflush(stdout);
         }
     }
-    size_t tb = (size_t)geo->numTexels * 16;
-    void *d_lm = nullptr, *d_tex = nullptr;
     if (rc == FMGI_OK && geo->numTexels > 0) {
-        if (hipMalloc(&d_lm, tb * 2) != hipSuccess || hipMalloc(&d_tex, tb) != hipSuccess) {
-            rc = set_err(FMGI_ERR_OOM, "texel buffers (%zu B)", tb * 3);
-        } else if (hipMemsetAsync(d_lm, 0, tb * 2, c->stream) != hipSuccess ||
-                   hipMemcpyAsync(d_tex, geo->texels, tb, hipMemcpyHostToDevice, c->stream) != hipSuccess) {
-            rc = set_err(FMGI_ERR_HIP, "texel upload");
+        /* launch every shard before waiting on any (all devices bake concurrently) */
+        for (int k = 0; k < nshard && rc == FMGI_OK; k++) {
+            fmgi_context *c = ctx[k];
+            if (hipSetDevice(c->device) != hipSuccess || hipMalloc(&lm[k], tb * 2) != hipSuccess) {
+                rc = set_err(FMGI_ERR_OOM, "lightmap buffer (%zu B) on device %d", tb * 2, c->device);
+                break;
+            }
+            if (hipMemsetAsync(lm[k], 0, tb * 2, c->stream) != hipSuccess) rc = set_err(FMGI_ERR_HIP, "memset");
+            uint64_t b = items * (uint64_t)k / (uint64_t)nshard, e = items * (uint64_t)(k + 1) / (uint64_t)nshard;
+            if (rc == FMGI_OK) rc = fmgi_bake_items(c, b, e, lm[k], kernel, c->stream);
         }
-        if (rc == FMGI_OK) rc = fmgi_bake_items(c, 0, items, d_lm, kernel, c->stream);
-        if (rc == FMGI_OK) rc = fmgi_finalize(c, d_lm, d_tex, d_tex, c->stream);
+        fmgi_context *c0 = ctx[0];
         if (rc == FMGI_OK) {
-            hipError_t e = hipMemcpyAsync(texels_out, d_tex, tb, hipMemcpyDeviceToHost, c->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            hipError_t e = hipSetDevice(c0->device);
+            if (e == hipSuccess) e = hipMalloc(&d_tex, tb);
+            if (e == hipSuccess) e = hipMemcpyAsync(d_tex, geo->texels, tb, hipMemcpyHostToDevice, c0->stream);
+            if (e == hipSuccess && nshard > 1) e = hipMalloc(&d_stage, tb * 2);
+            for (int k = 1; k < nshard && e == hipSuccess; k++) { /* sum shard k into shard 0 on GPU 0 */
+                e = hipStreamSynchronize(ctx[k]->stream);
+                if (e == hipSuccess)
+                    e = hipMemcpyPeerAsync(d_stage, c0->device, lm[k], ctx[k]->device, tb * 2, c0->stream);
+                if (e == hipSuccess)
+                    e = fmgi_launch_add_u64((unsigned long long *)lm[0], (const unsigned long long *)d_stage,
+                                            (int64_t)geo->numTexels * 4, c0->stream);
+            }
+            if (e != hipSuccess) rc = set_err(FMGI_ERR_HIP, "shard reduction: %s", hipGetErrorString(e));
+        }
+        if (rc == FMGI_OK) rc = fmgi_finalize(c0, lm[0], d_tex, d_tex, c0->stream);
+        if (rc == FMGI_OK) {
+            hipError_t e = hipMemcpyAsync(texels_out, d_tex, tb, hipMemcpyDeviceToHost, c0->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
             if (e != hipSuccess) rc = set_err(FMGI_ERR_HIP, "bake: %s", hipGetErrorString(e));
         }
     }
-    hipFree(d_lm);
-    hipFree(d_tex);
-    fmgi_destroy(c);
+    for (int k = 0; k < nshard; k++) {
+        if (!ctx[k]) continue;
+        if (hipSetDevice(ctx[k]->device) == hipSuccess) {
+            (void)hipStreamSynchronize(ctx[k]->stream);
+            (void)hipFree(lm[k]);
+            if (k == 0) {
+                (void)hipFree(d_tex);
+                (void)hipFree(d_stage);
+            }
+        }
+        fmgi_destroy(ctx[k]);
+    }
     return rc;
 }
 

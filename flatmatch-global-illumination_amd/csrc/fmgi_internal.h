@@ -47,7 +47,8 @@ struct BakeArgs {
     uint32_t *rng_final;
 };
 
-enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESCANS, KSTAT_TESTS, KSTAT_N = 8 };
+enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESCANS, KSTAT_TESTS, KSTAT_TIES,
+       KSTAT_INVALID, KSTAT_N };
 
 #define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
 
@@ -57,6 +58,7 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);
 hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long *colfx, unsigned long long *lm,
                                      int n, hipStream_t s);
+hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long *src, int64_t n, hipStream_t s);
 hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, float *tout, int64_t n,
                                 hipStream_t s);
 hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, hipStream_t s);

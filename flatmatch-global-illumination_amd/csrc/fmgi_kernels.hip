@@ -85,11 +85,18 @@ __device__ __forceinline__ float exact_at(const RectDev &r, f3 src, f3 dir, floa
 
 /* ---- scan policies -------------------------------------------------------------------------- */
 
+struct ScanStats {
+    unsigned long long tests = 0;    /* rectangle tests evaluated (phase-1 records + exact tests)   */
+    unsigned long long rescans = 0;  /* fast scan: scans re-done by the literal exact scan          */
+    unsigned long long ties = 0;     /*   ... because the runner-up was within the separation band */
+    unsigned long long invalid = 0;  /*   ... because the phase-1 winner failed the exact test     */
+};
+
 /* photonmap.cl:189-206, evaluated literally for every rectangle in index order. */
 struct ScanExact {
     static constexpr bool kLds = false;
     static __device__ __forceinline__ int scan(const BakeArgs &a, const char *, f3 src, f3 dir, float &best,
-                                               unsigned long long &tests, unsigned long long &) {
+                                               ScanStats &st) {
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         float bestd = INFINITY;
         int hit = -1;
@@ -98,7 +105,7 @@ struct ScanExact {
             if (d < 0) continue;
             if (d < bestd) { bestd = d; hit = i; }
         }
-        tests += (unsigned long long)a.nrects;
+        st.tests += (unsigned long long)a.nrects;
         best = bestd;
         return hit;
     }
@@ -153,7 +160,7 @@ __device__ __forceinline__ void filter_axis(const char *img, int J, f3 s, f3 d, 
 struct ScanFast {
     static constexpr bool kLds = true;
     static __device__ __forceinline__ int scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best,
-                                               unsigned long long &tests, unsigned long long &rescans) {
+                                               ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         filter_axis<0>(lds, a.fJ[0], src, dir, L1, L2, code1);
@@ -170,7 +177,7 @@ struct ScanFast {
             code1 = lt ? ((3 << 16) | g) : code1;
             L1 = lt ? key : L1;
         }
-        tests += (unsigned long long)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
+        st.tests += (unsigned long long)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
         if (L1 == INFINITY) { /* V is a subset of the (empty) phase-1 set: the photon escapes */
             best = INFINITY;
             return -1;
@@ -192,8 +199,9 @@ struct ScanFast {
             best = f;
             return idx;
         }
-        rescans++;
-        return ScanExact::scan(a, lds, src, dir, best, tests, rescans);
+        st.rescans++;
+        if (f < 0) st.invalid++; else st.ties++;
+        return ScanExact::scan(a, lds, src, dir, best, st);
     }
 };
 
@@ -240,7 +248,8 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
     bool win = false, alive = false;
     uint64_t item = 0;
     int nev = 0;
-    unsigned long long n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0, n_tests = 0, n_rescan = 0;
+    unsigned long long n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0;
+    ScanStats sst;
 
     for (;;) {
         if (!alive) {
@@ -281,7 +290,7 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         }
 
         float best;
-        int hit = Scan::scan(a, s_img, pos, dir, best, n_tests, n_rescan);
+        int hit = Scan::scan(a, s_img, pos, dir, best, sst);
         n_scan++;
         if (best == INFINITY) { /* photonmap.cl:208-209 */
             alive = false;
@@ -330,9 +339,9 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         a.rng_final[item - a.item_begin] = rng;
     }
 
-    unsigned long long v[6] = {n_ph, n_scan, n_dep, n_esc, n_rescan, n_tests};
+    unsigned long long v[KSTAT_N] = {n_ph, n_scan, n_dep, n_esc, sst.rescans, sst.tests, sst.ties, sst.invalid};
 #pragma unroll
-    for (int i = 0; i < 6; i++) {
+    for (int i = 0; i < KSTAT_N; i++) {
         unsigned long long s = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0 && s) atomicAdd(a.stats + i, s);
     }
@@ -375,6 +384,12 @@ __global__ void k_finalize(const unsigned long long *__restrict__ lm, const floa
     o.z = (float)((double)t.z + (double)q[2] * 2.98023223876953125e-08);
     o.w = t.w;
     tout[i] = o;
+}
+
+__global__ void k_add_u64(unsigned long long *__restrict__ dst, const unsigned long long *__restrict__ src,
+                          int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < n) dst[i] += src[i];
 }
 
 __global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, float *__restrict__ c, int64_t n) {
@@ -448,6 +463,12 @@ hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, 
     if (n <= 0) return hipSuccess;
     int64_t blocks = (n + 255) / 256;
     hipLaunchKernelGGL(k_finalize, dim3((unsigned)blocks), dim3(256), 0, s, lm, (const float4 *)tin, (float4 *)tout, n);
+    return hipGetLastError();
+}
+
+hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long *src, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_add_u64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
     return hipGetLastError();
 }
 

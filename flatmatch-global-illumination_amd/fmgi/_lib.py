@@ -53,11 +53,12 @@ class Stats(C.Structure):
         ("escapes", C.c_uint64),
         ("exact_rescans", C.c_uint64),
         ("tests", C.c_uint64),
-        ("reserved", C.c_uint64 * 2),
+        ("rescans_tie", C.c_uint64),
+        ("rescans_invalid", C.c_uint64),
     ]
 
     def as_dict(self):
-        return {k: int(getattr(self, k)) for k, _ in self._fields_ if k != "reserved"}
+        return {k: int(getattr(self, k)) for k, _ in self._fields_}
 
 
 class Geometry(C.Structure):

@@ -89,7 +89,8 @@ typedef struct fmgi_stats {
     uint64_t escapes;   /* scans that hit nothing (photonmap.cl:208)              */
     uint64_t exact_rescans; /* fast kernel: scans re-done by the exact scan          */
     uint64_t tests;     /* rectangle tests actually evaluated                      */
-    uint64_t reserved[2];
+    uint64_t rescans_tie;     /* exact_rescans caused by a runner-up within the separation band */
+    uint64_t rescans_invalid; /* exact_rescans caused by a phase-1 winner that is not exactly valid */
 } fmgi_stats;
 
 /* One work item of the flattened reference launch schedule (global_illumination_cl.c:246-267). */

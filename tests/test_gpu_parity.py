@@ -228,3 +228,19 @@ def test_reference_kernel_pins_oracle(torch_cuda, example_scene, offsets):
         same += np.array_equal(mine.view(np.uint32), ref[k].view(np.uint32))
     # recorded in tests/golden/ref_items_*.npz by make_ref_fixtures.py; most items must match exactly
     assert same >= 28, f"only {same}/32 work items bit-identical to the reference kernel"
+
+
+def test_multi_shard_drop_in_is_bit_identical(torch_cuda, box200, libc):
+    """performGlobalIlluminationCl sharded over FMGI_SHARDS work-item ranges (the multi-GPU path, here
+    round-robin on one device) reduces to exactly the single-shard texels."""
+    spa = 2_000_000
+    outs = []
+    for shards in ("1", "3"):
+        os.environ["FMGI_SHARDS"] = shards
+        try:
+            libc.srand(1)
+            outs.append(fmgi.bake_geometry(box200, spa))
+        finally:
+            del os.environ["FMGI_SHARDS"]
+    assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
+    assert outs[0][:, :3].sum() > 0
