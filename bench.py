@@ -96,6 +96,7 @@ def main():
                     help="none = PROFILING ONLY (deposits discarded; lightmap wrong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
+    ap.add_argument("--spa", type=int, default=0, help="override numSamplesPerArea of the config (per GPU)")
     args = ap.parse_args()
 
     import torch
@@ -113,7 +114,10 @@ def main():
     if world > 1:
         dist.init_process_group("nccl", device_id=torch.device("cuda", local))
 
-    cfg = CONFIGS[args.config]
+    cfg = dict(CONFIGS[args.config])
+    if args.spa:
+        cfg["spa"] = args.spa
+        cfg["desc"] += f" [spa overridden: {args.spa}]"
     sc = load_scene(cfg["scene"])
     spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
     spa = min(spa, 2**31 - 1)

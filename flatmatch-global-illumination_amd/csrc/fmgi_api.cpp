@@ -231,6 +231,9 @@ struct fmgi_context {
     LaunchDev *d_launches = nullptr;
     int64_t d_launch_cap = 0;
     uint64_t total_items = 0;
+    uint32_t launch_cap = 0;
+    uint64_t *d_src_item_begin = nullptr; /* [nsrc + 1] */
+    int32_t *d_src_launch0 = nullptr;     /* [nsrc]     */
     unsigned long long *d_counter = nullptr;
     unsigned long long *d_stats = nullptr;
     /* ScanFast filter image + non-axis-aligned rect list */
@@ -308,6 +311,8 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_launches);
     hipFree(c->d_fimg);
     hipFree(c->d_general);
+    hipFree(c->d_src_item_begin);
+    hipFree(c->d_src_launch0);
     hipFree(c->d_counts);
     hipFree(c->d_colfx);
     hipFree(c->d_counter);
@@ -465,7 +470,23 @@ FMGI_API int64_t fmgi_plan(fmgi_context *c, int spa, int wg, const int32_t *rng_
         c->d_launch_cap = (int64_t)L.size();
     }
     if (!L.empty()) HIPCHK(hipMemcpy(c->d_launches, L.data(), L.size() * sizeof(LaunchDev), hipMemcpyHostToDevice));
+    /* per-source lookup tables of the kernel's work-item -> launch mapping */
+    std::vector<uint64_t> sib((size_t)c->nsrcs + 1, item);
+    std::vector<int32_t> sl0((size_t)std::max(c->nsrcs, 1), (int32_t)L.size());
+    for (int64_t k = (int64_t)L.size() - 1; k >= 0; k--) {
+        sib[(size_t)L[k].source] = L[k].item_begin;
+        sl0[(size_t)L[k].source] = (int32_t)k;
     }
+    hipFree(c->d_src_item_begin);
+    hipFree(c->d_src_launch0);
+    c->d_src_item_begin = nullptr;
+    c->d_src_launch0 = nullptr;
+    HIPCHK(hipMalloc(&c->d_src_item_begin, sib.size() * sizeof(uint64_t)));
+    HIPCHK(hipMemcpy(c->d_src_item_begin, sib.data(), sib.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&c->d_src_launch0, sl0.size() * sizeof(int32_t)));
+    HIPCHK(hipMemcpy(c->d_src_launch0, sl0.data(), sl0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
+    }
+    c->launch_cap = (uint32_t)cap;
     c->h_launches.swap(L);
     c->total_items = item;
     if (total_items) *total_items = item;
@@ -507,6 +528,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.srcs = c->d_srcs;
     a.launches = c->d_launches;
     a.nlaunches = (int)c->h_launches.size();
+    a.src_item_begin = c->d_src_item_begin;
+    a.src_launch0 = c->d_src_launch0;
+    a.nsrc = c->nsrcs;
+    a.nwindows = c->nwindows;
+    a.launch_cap = c->launch_cap;
     a.item_begin = b;
     a.item_end = e;
     a.counter = c->d_counter;

@@ -26,6 +26,11 @@ struct BakeArgs {
     const SrcDev *srcs;
     const LaunchDev *launches;
     int nlaunches;
+    /* work item -> launch: per source, its first flattened item (nsrc + 1 entries) and first launch */
+    const uint64_t *src_item_begin;
+    const int32_t *src_launch0;
+    int nsrc, nwindows;
+    uint32_t launch_cap; /* WG * 100 items per reference launch */
     uint64_t item_begin, item_end;
     unsigned long long *counter;   /* work-item fetch counter, zeroed before each bake */
     unsigned long long *lm;        /* int64 fixed point [numTexels][4]                   */

@@ -43,22 +43,15 @@ constexpr LcgJumpC make_jump() {
     }
     return t;
 }
-__constant__ LcgJumpC c_jump = make_jump();
+constexpr LcgJumpC kJump = make_jump();
+__constant__ LcgJumpC c_jump = kJump;
+static_assert(kJump.a[1] == 1664525u && kJump.c[1] == 1013904223u, "LCG of photonmap.cl:23");
 
 struct EventDev {
     int32_t photon, depth, rect, texel;
     float rgb[3];
     uint32_t rng;
 };
-
-__device__ __forceinline__ int find_launch(const LaunchDev *__restrict__ L, int n, uint64_t item) {
-    int lo = 0, hi = n - 1;
-    while (lo < hi) {
-        int mid = (lo + hi + 1) >> 1;
-        if (L[mid].item_begin <= item) lo = mid; else hi = mid - 1;
-    }
-    return lo;
-}
 
 __device__ __forceinline__ unsigned long long fx(float v) {
     /* v >= 0.25 and a float => v * 2^25 is an integer < 2^53: exact */
@@ -233,6 +226,35 @@ struct AccNone {
 
 /* ---- the per-lane photon state machine ------------------------------------------------------- */
 
+/* flattened work item w -> (source, launch, gid): launches of one source are consecutive chunks of
+   launch_cap = WG*100 items (global_illumination_cl.c:255), so one search over the (few) sources and a
+   division replace a search over all launches */
+__device__ __forceinline__ void locate_item(const BakeArgs &a, uint64_t w, int &src, int &li, uint32_t &gid) {
+    int lo = 0, hi = a.nsrc - 1;
+    while (lo < hi) {
+        const int mid = (lo + hi + 1) >> 1;
+        if (a.src_item_begin[mid] <= w) lo = mid; else hi = mid - 1;
+    }
+    const uint64_t off = w - a.src_item_begin[lo];
+    src = lo;
+    li = a.src_launch0[lo] + (int)(off / a.launch_cap);
+    gid = (uint32_t)(off % a.launch_cap);
+}
+
+/* LCG^2: the two draws of a direction sample whose result is never used (last bounce) */
+__device__ __forceinline__ uint32_t lcg2(uint32_t s) {
+    constexpr uint32_t A2 = kJump.a[2], C2 = kJump.c[2];
+    return A2 * s + C2;
+}
+
+/*
+ * One loop iteration = [start a photon and/or sample a direction] -> [scan] -> [hit: deposit].
+ * Emission (photonmap.cl:173-181) and the diffuse bounce (:238) share ONE sample_dir call site, so a
+ * wave whose lanes are at different points of their photons (escapes, photonmap.cl:208) pays for one
+ * sampler per iteration, not two. The direction sampled at the last bounce (depth 8) is never used:
+ * its two draws are skipped with one LCG jump. Per lane, RNG draws happen in exactly the reference
+ * order: roulette (:236), bounce sample (:238), then the next photon's dx, dy (:173-174) and sample.
+ */
 template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
@@ -243,68 +265,81 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
     }
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
-    int depth = 0, left = 0, photon = -1, sid = 0;
-    int srci = 0;
-    bool win = false, alive = false;
+    f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
+    int depth = 0, left = 0, photon = -1, sid = 0, srci = 0;
+    bool win = false, start = true, pend = false;
     uint64_t item = 0;
     int nev = 0;
     unsigned long long n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0;
     ScanStats sst;
 
     for (;;) {
-        if (!alive) {
+        /* ---- stage 1: new photon (and new work item), then the iteration's one direction sample ---- */
+        float edx = 0, edy = 0;
+        if (start) {
             if (left == 0) {
                 if (TRACE && photon >= 0) {
                     a.ev_counts[item - a.item_begin] = nev;
                     a.rng_final[item - a.item_begin] = rng;
                 }
-                uint64_t w = a.item_begin + atomicAdd(a.counter, 1ull);
+                const uint64_t w = a.item_begin + atomicAdd(a.counter, 1ull);
                 if (w >= a.item_end) break;
                 item = w;
-                const LaunchDev L = a.launches[find_launch(a.launches, a.nlaunches, w)];
-                rng = (uint32_t)(w - L.item_begin) + (uint32_t)L.rng_offset;
-                /* photonmap.cl:272-275: r = rand()*40; ceil(r) further draws, as one LCG jump */
-                float r40 = rng_next(rng) * 40;
-                int k = (int)ceilf(r40);
+                int li;
+                uint32_t gid;
+                locate_item(a, w, srci, li, gid);
+                rng = gid + (uint32_t)a.launches[li].rng_offset; /* photonmap.cl:272 */
+                /* photonmap.cl:273-275: r = rand()*40; ceil(r) further draws, as one LCG jump */
+                const float r40 = rng_next(rng) * 40;
+                const int k = (int)ceilf(r40);
                 rng = c_jump.a[k] * rng + c_jump.c[k];
-                srci = L.source;
-                win = L.is_window != 0;
+                win = srci < a.nwindows;
                 left = FMGI_PHOTONS_PER_ITEM;
                 photon = -1;
                 nev = 0;
             }
-            /* photonmap.cl:167-181: emission */
             const SrcDev &S = a.srcs[srci];
-            col = win ? mkf3(18, 18, 18) : mkf3(16, 16, 18);
+            col = win ? mkf3(18, 18, 18) : mkf3(16, 16, 18); /* photonmap.cl:167-169 */
             sid = win ? (512 + 1) : 1; /* colour state: source kind, then one bit per diffuse bounce */
-            float dx = rng_next(rng);
-            float dy = rng_next(rng);
-            dir = sample_dir(rng, mkf3(S.nx, S.ny, S.nz), mkf3(S.bux, S.buy, S.buz), mkf3(S.bvx, S.bvy, S.bvz), win);
-            pos = add3(add3(add3(mkf3(S.px, S.py, S.pz), mul3(mkf3(S.wx, S.wy, S.wz), dx)), mul3(mkf3(S.hx, S.hy, S.hz), dy)),
-                       mul3(dir, 1e-5f));
+            edx = rng_next(rng);
+            edy = rng_next(rng);
+            sn = mkf3(S.nx, S.ny, S.nz);
+            sbu = mkf3(S.bux, S.buy, S.buz);
+            sbv = mkf3(S.bvx, S.bvy, S.bvz);
             left--;
             photon++;
             depth = 0;
-            alive = true;
             n_ph++;
         }
+        if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
+        if (start) {
+            const SrcDev &S = a.srcs[srci];
+            pos = add3(add3(add3(mkf3(S.px, S.py, S.pz), mul3(mkf3(S.wx, S.wy, S.wz), edx)),
+                            mul3(mkf3(S.hx, S.hy, S.hz), edy)),
+                       mul3(dir, 1e-5f));
+        } else {
+            pos = add3(pos, mul3(dir, 1e-5f)); /* photonmap.cl:261 (after the diffuse sample or the mirror) */
+        }
+        start = false;
+        pend = false;
 
+        /* ---- stage 2: scan ---- */
         float best;
-        int hit = Scan::scan(a, s_img, pos, dir, best, sst);
+        const int hit = Scan::scan(a, s_img, pos, dir, best, sst);
         n_scan++;
         if (best == INFINITY) { /* photonmap.cl:208-209 */
-            alive = false;
+            start = true;
             n_esc++;
             continue;
         }
-        /* photonmap.cl:216-258 */
+        /* ---- stage 3: hit (photonmap.cl:216-258) ---- */
         const RectDev &h = a.rects[hit];
         pos = add3(pos, mul3(dir, best));
         const f3 hn = mkf3(h.nx, h.ny, h.nz);
         const int texel = h.base + tile_at(mkf3(h.px, h.py, h.pz), mkf3(h.wnx, h.wny, h.wnz), h.wl,
                                            mkf3(h.hnx, h.hny, h.hnz), h.hl, h.W, h.H, pos);
+        const bool last = depth + 1 == FMGI_MAX_DEPTH;
         if ((double)pos.z > 0.0005 || rng_next(rng) > 0.75f) {
-            dir = sample_dir(rng, hn, mkf3(h.bux, h.buy, h.buz), mkf3(h.bvx, h.bvy, h.bvz), false);
             const bool floor = pos.z < 1e-5f;
             if (floor) {
                 col.y *= 0.85f;
@@ -312,8 +347,16 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
             }
             col = mul3(col, 0.9f);
             sid = (sid & 512) | ((sid & 511) << 1) | (floor ? 1 : 0);
+            if (last) {
+                rng = lcg2(rng); /* the direction of a photon that ends here is never used */
+            } else {
+                pend = true; /* sampled at the top of the next iteration */
+                sn = hn;
+                sbu = mkf3(h.bux, h.buy, h.buz);
+                sbv = mkf3(h.bvx, h.bvy, h.bvz);
+            }
         } else {
-            float two = 2.0f * dot3(hn, dir);
+            const float two = 2.0f * dot3(hn, dir);
             dir = sub3(dir, mul3(hn, two));
         }
         Acc::deposit(a, texel, sid, col);
@@ -327,12 +370,12 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
             e.rgb[0] = col.x;
             e.rgb[1] = col.y;
             e.rgb[2] = col.z;
-            e.rng = rng;
+            e.rng = pend ? lcg2(rng) : rng; /* RNG state after this bounce's sample */
             ((EventDev *)a.events)[(item - a.item_begin) * FMGI_EVENTS_PER_ITEM + nev] = e;
             nev++;
         }
-        pos = add3(pos, mul3(dir, 1e-5f));
-        if (++depth == FMGI_MAX_DEPTH) alive = false;
+        if (last) start = true;
+        depth++;
     }
     if (TRACE && photon >= 0) {
         a.ev_counts[item - a.item_begin] = nev;
