@@ -92,7 +92,7 @@ def main():
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
     ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
-    ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state", "none"],
+    ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state", "stream", "none"],
                     help="none = PROFILING ONLY (deposits discarded; lightmap wrong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
@@ -125,7 +125,7 @@ def main():
 
     ctx = fmgi.Context(local)
     ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE,
-                          "none": fmgi.ACCUM_NONE}[args.accum])
+                          "stream": fmgi.ACCUM_STREAM, "none": fmgi.ACCUM_NONE}[args.accum])
     ctx.set_scene(sc)
     libc = ctypes.CDLL(None)
     libc.srand(1)  # the unseeded state main.c runs with; every rank builds the same schedule
@@ -201,7 +201,7 @@ def main():
         # memory-side atomic adds issued per second by the bake (1 per deposit for the colour-state
         # counters, 3 for int64 RGB); ~20e9/s is the chip's rate for lane-scattered atomics
         # (MI355X_MICROARCH.md §Global float atomics: ~0.08 TB/s of 4-B adds)
-        per_dep = {1: 3, 2: 1, 3: 0}[ctx.accumulation]
+        per_dep = {1: 3, 2: 1, 3: 0, 4: 0}[ctx.accumulation]
         atomic_rate = per_dep * per_launch_deps / ks
         atomics = {"per_deposit": per_dep, "achieved_per_s": atomic_rate, "ceiling_per_s": 2.0e10,
                    "frac": atomic_rate / 2.0e10}
@@ -228,7 +228,8 @@ def main():
                 "spa": spa,
                 "photons_per_step": photons_per_step,
                 "kernel": args.kernel,
-                "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)"}[ctx.accumulation],
+                "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)",
+                                 4: "stream"}[ctx.accumulation],
                 "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
             },
             "roofline": {

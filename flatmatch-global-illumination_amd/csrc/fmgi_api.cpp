@@ -248,6 +248,10 @@ struct fmgi_context {
     int accum = FMGI_ACCUM_FX3;
     unsigned long long *d_counts = nullptr;
     long long *d_colfx = nullptr;
+    /* STREAM: deposit-code stream + fold buffers, grown on demand (fmgi_accum.hip) */
+    StreamBufs sb{};
+    uint64_t sb_cap_alloc = 0;
+    int sb_entries_alloc = 0;
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -289,8 +293,8 @@ FMGI_API fmgi_context *fmgi_create(int device) {
         c->num_cus = prop.multiProcessorCount;
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_counter, 64) != hipSuccess ||
-        hipMalloc(&c->d_stats, KSTAT_N * sizeof(unsigned long long)) != hipSuccess ||
-        hipMemset(c->d_stats, 0, KSTAT_N * sizeof(unsigned long long)) != hipSuccess) {
+        hipMalloc(&c->d_stats, KSTAT_ALLOC * sizeof(unsigned long long)) != hipSuccess ||
+        hipMemset(c->d_stats, 0, KSTAT_ALLOC * sizeof(unsigned long long)) != hipSuccess) {
         set_err(FMGI_ERR_HIP, "context allocation failed on device %d", device);
         fmgi_destroy(c);
         return nullptr;
@@ -315,6 +319,12 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_src_launch0);
     hipFree(c->d_counts);
     hipFree(c->d_colfx);
+    hipFree(c->sb.stream);
+    hipFree(c->sb.sorted);
+    hipFree(c->sb.cursor);
+    hipFree(c->sb.hist);
+    hipFree(c->sb.offs);
+    hipFree(c->sb.scan_tmp);
     hipFree(c->d_counter);
     hipFree(c->d_stats);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -324,28 +334,81 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
 /* AccState needs 8 KiB of u64 counters per texel; above this budget (or on request) AccFx3 is used. */
 static const size_t kStateBudget = (size_t)8 << 30;
 
+static const int kStreamMaxTexels = FMGI_MAX_TILES << FMGI_TILE_BITS; /* 4,194,304; also keeps codes != ~0u */
+
+static int ensure_colour_table(fmgi_context *c) {
+    if (c->d_colfx) return FMGI_OK;
+    std::vector<long long> t = colour_table();
+    HIPCHK(hipMalloc(&c->d_colfx, t.size() * sizeof(long long)));
+    HIPCHK(hipMemcpy(c->d_colfx, t.data(), t.size() * sizeof(long long), hipMemcpyHostToDevice));
+    return FMGI_OK;
+}
+
 static int configure_accum(fmgi_context *c) {
     size_t bytes = (size_t)FMGI_COLOUR_STATES * (size_t)c->num_texels * sizeof(unsigned long long);
     int want = c->accum_req;
-    if (want == FMGI_ACCUM_AUTO) want = (bytes && bytes <= kStateBudget) ? FMGI_ACCUM_STATE : FMGI_ACCUM_FX3;
+    if (want == FMGI_ACCUM_AUTO)
+        want = (c->num_texels > 0 && c->num_texels < kStreamMaxTexels) ? FMGI_ACCUM_STREAM : FMGI_ACCUM_FX3;
+    if (want == FMGI_ACCUM_STREAM && c->num_texels >= kStreamMaxTexels) want = FMGI_ACCUM_FX3;
     hipFree(c->d_counts);
     c->d_counts = nullptr;
     c->accum = want == FMGI_ACCUM_NONE ? FMGI_ACCUM_NONE : FMGI_ACCUM_FX3;
-    if (want != FMGI_ACCUM_STATE || !bytes) return FMGI_OK;
     HIPCHK(hipSetDevice(c->device));
+    if (want == FMGI_ACCUM_STREAM) {
+        int rc = ensure_colour_table(c);
+        if (rc != FMGI_OK) return rc;
+        c->accum = FMGI_ACCUM_STREAM;
+        return FMGI_OK;
+    }
+    if (want != FMGI_ACCUM_STATE || !bytes) return FMGI_OK;
     HIPCHK(hipMalloc(&c->d_counts, bytes));
     HIPCHK(hipMemset(c->d_counts, 0, bytes));
-    if (!c->d_colfx) {
-        std::vector<long long> t = colour_table();
-        HIPCHK(hipMalloc(&c->d_colfx, t.size() * sizeof(long long)));
-        HIPCHK(hipMemcpy(c->d_colfx, t.data(), t.size() * sizeof(long long), hipMemcpyHostToDevice));
-    }
+    int rc = ensure_colour_table(c);
+    if (rc != FMGI_OK) return rc;
     c->accum = FMGI_ACCUM_STATE;
     return FMGI_OK;
 }
 
+/* STREAM buffers for a bake of `items` work items on `grid` blocks of `block` lanes: every item makes at
+   most 800 deposits and every wave wastes at most one partly filled block. */
+static int ensure_stream(fmgi_context *c, uint64_t items, int grid, int block) {
+    const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
+    const uint64_t cap = items * FMGI_EVENTS_PER_ITEM + (waves + 1) * FMGI_STREAM_BLOCK;
+    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
+    const uint64_t nslices = (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
+    const uint64_t entries = (uint64_t)P * nslices + 1;
+    if (entries > (uint64_t)INT32_MAX) return set_err(FMGI_ERR_ARG, "stream fold too large (%llu entries)",
+                                                     (unsigned long long)entries);
+    if (cap > c->sb_cap_alloc) {
+        hipFree(c->sb.stream);
+        hipFree(c->sb.sorted);
+        c->sb.stream = c->sb.sorted = nullptr;
+        c->sb_cap_alloc = 0;
+        HIPCHK(hipMalloc(&c->sb.stream, cap * sizeof(uint32_t)));
+        HIPCHK(hipMalloc(&c->sb.sorted, cap * sizeof(uint32_t)));
+        c->sb_cap_alloc = cap;
+    }
+    if ((int)entries > c->sb_entries_alloc) {
+        hipFree(c->sb.hist);
+        hipFree(c->sb.offs);
+        hipFree(c->sb.scan_tmp);
+        c->sb.hist = c->sb.offs = nullptr;
+        c->sb.scan_tmp = nullptr;
+        c->sb_entries_alloc = 0;
+        HIPCHK(hipMalloc(&c->sb.hist, entries * sizeof(unsigned long long)));
+        HIPCHK(hipMalloc(&c->sb.offs, entries * sizeof(unsigned long long)));
+        c->sb.scan_tmp_bytes = fmgi_stream_scan_bytes((int)entries);
+        HIPCHK(hipMalloc(&c->sb.scan_tmp, std::max<size_t>(c->sb.scan_tmp_bytes, 16)));
+        c->sb_entries_alloc = (int)entries;
+    }
+    if (!c->sb.cursor) HIPCHK(hipMalloc(&c->sb.cursor, 64));
+    c->sb.cap = cap;
+    c->sb.accum_blocks = c->num_cus * 2;
+    return FMGI_OK;
+}
+
 FMGI_API int fmgi_set_accumulation(fmgi_context *c, int mode) {
-    if (!c || mode < FMGI_ACCUM_AUTO || mode > FMGI_ACCUM_NONE) return set_err(FMGI_ERR_ARG, "bad accumulation mode");
+    if (!c || mode < FMGI_ACCUM_AUTO || mode > FMGI_ACCUM_STREAM) return set_err(FMGI_ERR_ARG, "bad accumulation mode");
     c->accum_req = mode;
     if (c->device == FMGI_HOST_ONLY || c->num_texels == 0) return FMGI_OK;
     return configure_accum(c);
@@ -548,12 +611,35 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.events = events;
     a.ev_counts = counts;
     a.rng_final = rngf;
+    a.overflow = c->d_stats + KSTAT_OVERFLOW;
     const int block = 256;
-    HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
-    HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid_blocks(c, kernel, c->accum, trace, block, e - b), block, s));
-    /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
-    if (a.counts)
-        HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
+    if (c->accum != FMGI_ACCUM_STREAM) {
+        HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
+        HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid_blocks(c, kernel, c->accum, trace, block, e - b),
+                                block, s));
+        /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
+        if (a.counts)
+            HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
+        return FMGI_OK;
+    }
+    /* STREAM: at most kStreamChunkItems work items (4e8 photons; <= 12.8 GB of codes at the worst case
+       of 8 deposits per photon) per stream */
+    const uint64_t kStreamChunkItems = 4000000;
+    for (uint64_t cb = b; cb < e; cb += kStreamChunkItems) {
+        const uint64_t ce = std::min(e, cb + kStreamChunkItems);
+        const int grid = grid_blocks(c, kernel, c->accum, trace, block, ce - cb);
+        int rc = ensure_stream(c, ce - cb, grid, block);
+        if (rc != FMGI_OK) return rc;
+        a.item_begin = cb;
+        a.item_end = ce;
+        a.stream = c->sb.stream;
+        a.stream_cap = c->sb.cap;
+        a.stream_cursor = c->sb.cursor;
+        HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
+        HIPCHK(hipMemsetAsync(c->sb.cursor, 0, 8, s));
+        HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid, block, s));
+        HIPCHK(fmgi_stream_fold(c->sb, c->num_texels, c->d_colfx, (unsigned long long *)lm, s));
+    }
     return FMGI_OK;
 }
 
@@ -578,7 +664,7 @@ FMGI_API int fmgi_get_stats(fmgi_context *c, fmgi_stats *out) {
     if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
-    unsigned long long v[KSTAT_N];
+    unsigned long long v[KSTAT_ALLOC];
     HIPCHK(hipMemcpy(v, c->d_stats, sizeof v, hipMemcpyDeviceToHost));
     memset(out, 0, sizeof *out);
     out->photons = v[KSTAT_PHOTONS];
@@ -589,6 +675,7 @@ FMGI_API int fmgi_get_stats(fmgi_context *c, fmgi_stats *out) {
     out->tests = v[KSTAT_TESTS];
     out->rescans_tie = v[KSTAT_TIES];
     out->rescans_invalid = v[KSTAT_INVALID];
+    out->stream_overflow = v[KSTAT_OVERFLOW];
     return FMGI_OK;
 }
 
@@ -597,7 +684,7 @@ FMGI_API int fmgi_reset_stats(fmgi_context *c) {
     if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemset(c->d_stats, 0, KSTAT_N * sizeof(unsigned long long)));
+    HIPCHK(hipMemset(c->d_stats, 0, KSTAT_ALLOC * sizeof(unsigned long long)));
     return FMGI_OK;
 }
 

@@ -45,6 +45,12 @@ struct BakeArgs {
     int ngeneral;
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
     unsigned long long *counts;
+    /* AccStream accumulation: deposit codes (texel << 10 | colour state) appended to stream[0..cap) in
+       blocks of FMGI_STREAM_BLOCK codes reserved through stream_cursor (fmgi_accum.hip) */
+    uint32_t *stream;
+    uint64_t stream_cap;
+    unsigned long long *stream_cursor;
+    unsigned long long *overflow; /* set if a reservation would pass stream_cap (never, by sizing) */
     int num_texels;
     /* debug trace (TRACE kernels only) */
     void *events;                  /* fmgi_event[(item - item_begin) * 800 + k]                     */
@@ -53,11 +59,32 @@ struct BakeArgs {
 };
 
 enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESCANS, KSTAT_TESTS, KSTAT_TIES,
-       KSTAT_INVALID, KSTAT_N };
+       KSTAT_INVALID, KSTAT_N, KSTAT_OVERFLOW = KSTAT_N, KSTAT_ALLOC = 16 };
+
+/* stream accumulation geometry (fmgi_accum.hip) */
+#define FMGI_STREAM_BLOCK 4096 /* codes reserved per wave at a time                         */
+#define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
+#define FMGI_TILE_BITS 12      /* 4096-texel tiles summed in LDS                              */
+#define FMGI_MAX_TILES 1024    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */
+
+struct StreamBufs {
+    uint32_t *stream;               /* deposit codes, cap entries                     */
+    uint64_t cap;
+    unsigned long long *cursor;     /* reserved codes (device)                        */
+    uint32_t *sorted;               /* codes sorted by tile, cap entries              */
+    unsigned long long *hist;       /* [tiles * slices + 1] counts, then ...          */
+    unsigned long long *offs;       /* ... their exclusive scan                       */
+    void *scan_tmp;
+    size_t scan_tmp_bytes;
+    int accum_blocks;
+};
+hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, const long long *colfx, unsigned long long *lm,
+                            hipStream_t s);
+size_t fmgi_stream_scan_bytes(int entries);
 
 #define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
 
-/* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only) */
+/* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only), 4 = AccStream */
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);

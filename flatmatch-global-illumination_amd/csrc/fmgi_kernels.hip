@@ -224,6 +224,66 @@ struct AccNone {
     static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
 };
 
+/* Deposits become codes (texel << 10 | colour state) appended to a stream (fmgi_accum.hip folds it).
+   The append is a wave-level operation at the end of each loop iteration, where every live lane of the
+   wave is active: the depositing lanes get consecutive slots (ballot + mbcnt), so one iteration's codes
+   are one coalesced store; one lane reserves a new FMGI_STREAM_BLOCK-code block when the current one
+   fills (the wave-uniform [wbase, wend) is kept identical in every live lane). */
+struct WaveStream {
+    uint64_t base = 0, end = 0;
+};
+
+struct AccStream {
+    static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
+    static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, bool dep, uint32_t code) {
+        const uint64_t m = __ballot(dep);
+        if (m == 0) return;
+        const uint32_t n = (uint32_t)__popcll(m);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint64_t room = ws.end - ws.base;
+        if (n <= room) {
+            if (dep) a.stream[ws.base + r] = code;
+            ws.base += n;
+            return;
+        }
+        if (dep && r < room) a.stream[ws.base + r] = code;
+        /* one lane reserves the next block; every live lane learns its base */
+        const uint64_t live = __ballot(true);
+        const int leader = __ffsll((long long)live) - 1;
+        unsigned long long nb = 0;
+        if ((int)__lane_id() == leader) {
+            nb = atomicAdd(a.stream_cursor, (unsigned long long)FMGI_STREAM_BLOCK);
+            if (nb + FMGI_STREAM_BLOCK > a.stream_cap) atomicAdd(a.overflow, 1ull);
+        }
+        nb = __shfl(nb, leader, 64);
+        ws.base = nb;
+        ws.end = nb + FMGI_STREAM_BLOCK;
+        if (ws.end > a.stream_cap) ws.end = ws.base; /* (never by sizing) drop instead of writing out of bounds */
+        if (dep && r >= room && ws.base + (r - room) < ws.end) a.stream[ws.base + (r - room)] = code;
+        ws.base += n - room;
+        if (ws.base > ws.end) ws.base = ws.end;
+    }
+    /* after the loop (all lanes of the wave reconverged): pad the wave's last block with sentinels */
+    static __device__ __forceinline__ void finish(const BakeArgs &a, WaveStream &ws) {
+        uint64_t b = ws.base, e = ws.end;
+        for (int off = 32; off > 0; off >>= 1) { /* lanes that left early hold older (smaller) values */
+            const uint64_t ob = __shfl_xor(b, off, 64), oe = __shfl_xor(e, off, 64);
+            b = ob > b ? ob : b;
+            e = oe > e ? oe : e;
+        }
+        for (uint64_t k = b + __lane_id(); k < e; k += 64) a.stream[k] = 0xFFFFFFFFu;
+    }
+};
+
+template <class Acc>
+struct HasAppend {
+    static constexpr bool value = false;
+};
+template <>
+struct HasAppend<AccStream> {
+    static constexpr bool value = true;
+};
+
 /* ---- the per-lane photon state machine ------------------------------------------------------- */
 
 /* flattened work item w -> (source, launch, gid): launches of one source are consecutive chunks of
@@ -272,6 +332,7 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
     int nev = 0;
     unsigned long long n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0;
     ScanStats sst;
+    WaveStream ws;
 
     for (;;) {
         /* ---- stage 1: new photon (and new work item), then the iteration's one direction sample ---- */
@@ -327,11 +388,12 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         float best;
         const int hit = Scan::scan(a, s_img, pos, dir, best, sst);
         n_scan++;
+        bool dep = false;
+        uint32_t code = 0;
         if (best == INFINITY) { /* photonmap.cl:208-209 */
             start = true;
             n_esc++;
-            continue;
-        }
+        } else {
         /* ---- stage 3: hit (photonmap.cl:216-258) ---- */
         const RectDev &h = a.rects[hit];
         pos = add3(pos, mul3(dir, best));
@@ -360,6 +422,8 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
             dir = sub3(dir, mul3(hn, two));
         }
         Acc::deposit(a, texel, sid, col);
+        dep = true;
+        code = ((uint32_t)texel << 10) | (uint32_t)sid;
         n_dep++;
         if (TRACE) {
             EventDev e;
@@ -376,7 +440,10 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         }
         if (last) start = true;
         depth++;
+        }
+        if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, dep, code);
     }
+    if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws);
     if (TRACE && photon >= 0) {
         a.ev_counts[item - a.item_begin] = nev;
         a.rng_final[item - a.item_begin] = rng;
@@ -461,10 +528,12 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
     if (kernel == 1) {
         if (accum == 2) return kernel_ptr<ScanFast, AccState>(trace);
         if (accum == 3) return kernel_ptr<ScanFast, AccNone>(trace);
+        if (accum == 4) return kernel_ptr<ScanFast, AccStream>(trace);
         return kernel_ptr<ScanFast, AccFx3>(trace);
     }
     if (accum == 2) return kernel_ptr<ScanExact, AccState>(trace);
     if (accum == 3) return kernel_ptr<ScanExact, AccNone>(trace);
+    if (accum == 4) return kernel_ptr<ScanExact, AccStream>(trace);
     return kernel_ptr<ScanExact, AccFx3>(trace);
 }
 
@@ -485,10 +554,12 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
     if (kernel == 1) { /* FMGI_KERNEL_FAST */
         if (accum == 2) launch3<ScanFast, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanFast, AccNone>(a, trace, grid, blk, lds, s);
+        else if (accum == 4) launch3<ScanFast, AccStream>(a, trace, grid, blk, lds, s);
         else launch3<ScanFast, AccFx3>(a, trace, grid, blk, lds, s);
     } else {
         if (accum == 2) launch3<ScanExact, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanExact, AccNone>(a, trace, grid, blk, lds, s);
+        else if (accum == 4) launch3<ScanExact, AccStream>(a, trace, grid, blk, lds, s);
         else launch3<ScanExact, AccFx3>(a, trace, grid, blk, lds, s);
     }
     return hipGetLastError();

@@ -18,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import scene
-from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, KERNEL_EXACT, KERNEL_FAST, FmgiError, Geometry, Stats,
+from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_EXACT, KERNEL_FAST, FmgiError, Geometry, Stats,
                    check, load)
 from .scene import RECT_DTYPE, Scene
 
@@ -45,6 +45,7 @@ __all__ = [
     "ACCUM_AUTO",
     "ACCUM_FX3",
     "ACCUM_STATE",
+    "ACCUM_STREAM",
     "LAUNCH_DTYPE",
     "EVENT_DTYPE",
     "device_count",

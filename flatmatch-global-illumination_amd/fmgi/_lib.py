@@ -39,6 +39,7 @@ ACCUM_AUTO = 0
 ACCUM_FX3 = 1
 ACCUM_STATE = 2
 ACCUM_NONE = 3  # profiling only: deposits discarded
+ACCUM_STREAM = 4
 
 
 class FmgiError(RuntimeError):
@@ -55,6 +56,7 @@ class Stats(C.Structure):
         ("tests", C.c_uint64),
         ("rescans_tie", C.c_uint64),
         ("rescans_invalid", C.c_uint64),
+        ("stream_overflow", C.c_uint64),
     ]
 
     def as_dict(self):

@@ -77,9 +77,12 @@ enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1 };
    FX3   three int64 fixed-point atomics per deposit into the lightmap;
    STATE one u64 atomic per deposit into counts[colour state][texel] (8 KiB per texel of device memory),
          folded into the int64 lightmap at the end of every fmgi_bake_items;
-   AUTO  STATE when the counters fit an 8 GiB budget, else FX3;
+   STREAM no atomics per deposit: 32-bit codes (texel << 10 | colour state) appended with coalesced
+         stores, then partitioned by 4096-texel tile and summed exactly in LDS (needs < 4,194,304 texels
+         and 2 x 12.8 GB of device memory: bakes run in chunks of 4e8 photons);
+   AUTO  STREAM when the texel count allows it, else FX3;
    NONE  PROFILING ONLY: deposits are discarded (measures the tracing work alone; wrong lightmap). */
-enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2, FMGI_ACCUM_NONE = 3 };
+enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2, FMGI_ACCUM_NONE = 3, FMGI_ACCUM_STREAM = 4 };
 
 /* Per-bake counters, accumulated on the device (one atomic per wave). */
 typedef struct fmgi_stats {
@@ -91,6 +94,7 @@ typedef struct fmgi_stats {
     uint64_t tests;     /* rectangle tests actually evaluated                      */
     uint64_t rescans_tie;     /* exact_rescans caused by a runner-up within the separation band */
     uint64_t rescans_invalid; /* exact_rescans caused by a phase-1 winner that is not exactly valid */
+    uint64_t stream_overflow; /* STREAM: reservations past the stream capacity (must stay 0) */
 } fmgi_stats;
 
 /* One work item of the flattened reference launch schedule (global_illumination_cl.c:246-267). */

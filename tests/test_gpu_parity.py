@@ -111,7 +111,7 @@ def test_per_photon_traces_boxes(torch_cuda, box200, box2000, offsets, kernel):
         ctx.close()
 
 
-ACCUMS = [fmgi.ACCUM_FX3, fmgi.ACCUM_STATE]
+ACCUMS = [fmgi.ACCUM_FX3, fmgi.ACCUM_STATE, fmgi.ACCUM_STREAM]
 
 
 @pytest.mark.parametrize("accum", ACCUMS)
@@ -157,8 +157,15 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     b2 = _bake_gpu(torch_cuda, ctx, n // 3, n, fmgi.KERNEL_FAST)
     ctx.set_accumulation(fmgi.ACCUM_FX3)
     c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
+    ctx.set_accumulation(fmgi.ACCUM_STREAM)
+    d = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)  # 3 chunks of <= 4e6 items
+    d1 = _bake_gpu(torch_cuda, ctx, 0, 12_345, fmgi.KERNEL_FAST)
+    d2 = _bake_gpu(torch_cuda, ctx, 12_345, n, fmgi.KERNEL_FAST)
     assert np.array_equal(a, b1 + b2)
-    assert np.array_equal(a, c)  # the two accumulation modes agree bit for bit
+    assert np.array_equal(a, c)  # the accumulation modes agree bit for bit
+    assert np.array_equal(a, d)
+    assert np.array_equal(a, d1 + d2)
+    assert ctx.stats()["stream_overflow"] == 0
     ctx.reset_stats()
     _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
     st = ctx.stats()
