@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", default="fast", choices=["fast", "exact"])
+    ap.add_argument("--kernel", default="grid", choices=["grid", "fast", "exact"])
     ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state", "stream", "none"],
                     help="none = PROFILING ONLY (deposits discarded; lightmap wrong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -121,7 +121,7 @@ def main():
     sc = load_scene(cfg["scene"])
     spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
     spa = min(spa, 2**31 - 1)
-    kernel = fmgi.KERNEL_FAST if args.kernel == "fast" else fmgi.KERNEL_EXACT
+    kernel = {"grid": fmgi.KERNEL_GRID, "fast": fmgi.KERNEL_FAST, "exact": fmgi.KERNEL_EXACT}[args.kernel]
 
     ctx = fmgi.Context(local)
     ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE,

@@ -38,13 +38,16 @@ __global__ __launch_bounds__(256) void k_tile_hist(const uint32_t *__restrict__ 
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
     const uint64_t b0 = (uint64_t)blockIdx.x * kSlice;
     if (b0 >= n) return; /* uniform; hist was zeroed */
-    for (int k = threadIdx.x; k < kSlice; k += blockDim.x) {
-        const uint64_t i = b0 + k;
-        if (i < n) {
-            const uint32_t c = stream[i];
-            if (c != kSentinel) atomicAdd(&h[tile_of(c)], 1u);
-        }
+    constexpr int per = kSlice / 256;
+    uint32_t c[per];
+#pragma unroll
+    for (int k = 0; k < per; k++) { /* all loads in flight before the first LDS atomic */
+        const uint64_t i = b0 + (uint64_t)k * 256 + threadIdx.x;
+        c[k] = i < n ? stream[i] : kSentinel;
     }
+#pragma unroll
+    for (int k = 0; k < per; k++)
+        if (c[k] != kSentinel) atomicAdd(&h[tile_of(c[k])], 1u);
     __syncthreads();
     for (int t = threadIdx.x; t < P; t += blockDim.x) hist[(size_t)t * nslices + blockIdx.x] = h[t];
 }
@@ -80,19 +83,25 @@ __global__ __launch_bounds__(256) void k_tile_scatter(const uint32_t *__restrict
                                                      uint32_t *__restrict__ sorted) {
     __shared__ uint32_t buf[kSlice];
     __shared__ uint32_t cnt[FMGI_MAX_TILES], loc[FMGI_MAX_TILES];
+    __shared__ unsigned long long dst[FMGI_MAX_TILES]; /* this slice's run start of each tile */
     constexpr int per = kSlice / 256;
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
     const uint64_t b0 = (uint64_t)blockIdx.x * kSlice;
     if (b0 >= n) return; /* uniform: the whole block is past the end */
-    for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[i] = 0;
+    for (int i = threadIdx.x; i < P; i += blockDim.x) {
+        cnt[i] = 0;
+        dst[i] = offs[(size_t)i * nslices + blockIdx.x];
+    }
     __syncthreads();
     uint32_t c[per];
 #pragma unroll
     for (int k = 0; k < per; k++) {
         const uint64_t i = b0 + (uint64_t)k * 256 + threadIdx.x;
         c[k] = i < n ? stream[i] : kSentinel;
-        if (c[k] != kSentinel) atomicAdd(&cnt[tile_of(c[k])], 1u);
     }
+#pragma unroll
+    for (int k = 0; k < per; k++)
+        if (c[k] != kSentinel) atomicAdd(&cnt[tile_of(c[k])], 1u);
     __syncthreads();
     block_exclusive_scan(cnt, loc, P);
     /* counting sort into LDS: cnt becomes the running cursor of each tile */
@@ -106,7 +115,7 @@ __global__ __launch_bounds__(256) void k_tile_scatter(const uint32_t *__restrict
     for (int k = threadIdx.x; k < total; k += blockDim.x) {
         const uint32_t v = buf[k];
         const int t = tile_of(v);
-        sorted[offs[(size_t)t * nslices + blockIdx.x] + (uint64_t)(k - (int)loc[t])] = v;
+        sorted[dst[t] + (uint64_t)(k - (int)loc[t])] = v;
     }
 }
 
@@ -136,13 +145,23 @@ __global__ __launch_bounds__(1024) void k_tile_accum(const uint32_t *__restrict_
         if (s0 >= s1) continue;
         for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) acc[i] = 0;
         __syncthreads();
-        for (uint64_t i = s0 + threadIdx.x; i < s1; i += blockDim.x) {
-            const uint32_t v = sorted[i];
-            const int tx = (int)((v >> 10) & (kTileTexels - 1));
-            const int sid = (int)(v & 1023);
-            atomicAdd(&acc[3 * tx + 0], (unsigned long long)col[3 * sid + 0]);
-            atomicAdd(&acc[3 * tx + 1], (unsigned long long)col[3 * sid + 1]);
-            atomicAdd(&acc[3 * tx + 2], (unsigned long long)col[3 * sid + 2]);
+        constexpr int U = 4; /* loads in flight per thread */
+        for (uint64_t i0 = s0 + threadIdx.x; i0 < s1; i0 += (uint64_t)U * blockDim.x) {
+            uint32_t v[U];
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                const uint64_t i = i0 + (uint64_t)u * blockDim.x;
+                v[u] = i < s1 ? sorted[i] : kSentinel;
+            }
+#pragma unroll
+            for (int u = 0; u < U; u++) {
+                if (v[u] == kSentinel) continue;
+                const int tx = (int)((v[u] >> 10) & (kTileTexels - 1));
+                const int sid = (int)(v[u] & 1023);
+                atomicAdd(&acc[3 * tx + 0], (unsigned long long)col[3 * sid + 0]);
+                atomicAdd(&acc[3 * tx + 1], (unsigned long long)col[3 * sid + 1]);
+                atomicAdd(&acc[3 * tx + 2], (unsigned long long)col[3 * sid + 2]);
+            }
         }
         __syncthreads();
         for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) {

@@ -115,6 +115,8 @@ struct FilterBuild {
     int J[3] = {0, 0, 0};
     std::vector<int32_t> general;
     float margin = 0;
+    double scale = 1; /* B: scene scale the margin is derived from */
+    std::vector<FilterRec> cls[3][2]; /* axis-aligned records by (axis, class), rect order */
 };
 
 int nonzero_axis(const float *v) {
@@ -151,7 +153,8 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
     }
     double B = std::max(std::max(S, sqrt(D2)), 1.0);
     fb.margin = (float)(B * (1.0 / 131072.0));
-    std::vector<FilterRec> cls[3][2];
+    fb.scale = B;
+    std::vector<FilterRec>(&cls)[3][2] = fb.cls;
     for (int i = 0; i < nw; i++) {
         const fmgi_rect &r = walls[i];
         int a = nonzero_axis(r.n.s), aw = nonzero_axis(r.width.s), ah = nonzero_axis(r.height.s);
@@ -189,6 +192,158 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
     }
     if (fb.img.empty()) fb.img.push_back(sentinel);
     return fb;
+}
+
+template <class T>
+hipError_t upload(T **dst, const std::vector<T> &v) {
+    hipError_t e = hipMalloc(dst, v.size() * sizeof(T));
+    if (e != hipSuccess) return e;
+    return hipMemcpy(*dst, v.data(), v.size() * sizeof(T), hipMemcpyHostToDevice);
+}
+
+/*
+ * Grid tables for ScanGrid (fmgi_kernels.hip). The records of each (axis, class) are grouped by plane
+ * (identical float plane coordinate, so identical phase-1 fac'), and each plane's records are bucketed
+ * by a uniform nu x nv grid over the bounding box of their grown extents (about 2 cells per record).
+ * A record is registered in every cell its grown extent [c - hw, c + hw] overlaps, widened by `slack`
+ * cells: the kernel's float cell coordinate t = (x - u0) * iu is within far less than that of the exact
+ * value for any x in the scene box, so a hit point inside a record's grown extent always lands in a cell
+ * that lists the record. Cell 0 is an empty cell used by the padding planes.
+ */
+struct GridBuild {
+    std::vector<GridPlane> img; /* per axis a: J[a] pairs {+a plane j, -a plane j} */
+    int J[3] = {0, 0, 0};
+    std::vector<uint32_t> cells; /* {start, count} pairs */
+    std::vector<float> recs;     /* {cu, hwu, cv, hwv} per cell entry */
+    std::vector<int32_t> idx;
+};
+
+GridBuild build_grid(const FilterBuild &fb) {
+    GridBuild gb;
+    gb.cells = {0u, 0u};
+    std::vector<GridPlane> planes[3][2];
+    for (int a = 0; a < 3; a++) {
+        for (int c = 0; c < 2; c++) {
+            const std::vector<FilterRec> &L = fb.cls[a][c];
+            std::vector<float> keys;
+            for (const FilterRec &r : L)
+                if (std::find_if(keys.begin(), keys.end(), [&](float k) { return memcmp(&k, &r.plane, 4) == 0; }) ==
+                    keys.end())
+                    keys.push_back(r.plane);
+            for (float pk : keys) {
+                std::vector<const FilterRec *> R;
+                for (const FilterRec &r : L)
+                    if (memcmp(&pk, &r.plane, 4) == 0) R.push_back(&r);
+                double ulo = 1e300, uhi = -1e300, vlo = 1e300, vhi = -1e300;
+                for (const FilterRec *r : R) {
+                    ulo = std::min(ulo, (double)r->cu - r->hwu);
+                    uhi = std::max(uhi, (double)r->cu + r->hwu);
+                    vlo = std::min(vlo, (double)r->cv - r->hwv);
+                    vhi = std::max(vhi, (double)r->cv + r->hwv);
+                }
+                const double eu = std::max(uhi - ulo, 1e-30), ev = std::max(vhi - vlo, 1e-30);
+                auto lo_hi = [](double c, double hw, double o, double inv, double sl, int n, int &i0, int &i1) {
+                    i0 = (int)std::floor((c - hw - o) * inv - sl);
+                    i1 = (int)std::floor((c + hw - o) * inv + sl);
+                    i0 = std::min(std::max(i0, 0), n - 1);
+                    i1 = std::min(std::max(i1, 0), n - 1);
+                };
+                /* one axis of the grid: n cells of size e/m starting half a cell early when `half`
+                   (so that rect edges on a regular lattice fall inside cells, not on their borders) */
+                struct Axis {
+                    float o, inv;
+                    int n;
+                    double slack;
+                    std::vector<int> cnt; /* cells each record is registered in */
+                };
+                auto make_axis = [&](double lo, double e, int m, bool half, bool is_u) {
+                    Axis ax;
+                    const double cs = e / m;
+                    ax.o = (float)(half ? lo - 0.5 * cs : lo);
+                    ax.inv = (float)(1.0 / cs);
+                    ax.n = m + (half ? 1 : 0);
+                    /* slack in cells: float rounding of (x - o) and of the product, for |x| <= scale */
+                    ax.slack = 1.0 / 64 + fb.scale * (double)ax.inv * 0x1p-18;
+                    for (const FilterRec *r : R) {
+                        int i0, i1;
+                        lo_hi(is_u ? r->cu : r->cv, is_u ? r->hwu : r->hwv, ax.o, ax.inv, ax.slack, ax.n, i0, i1);
+                        ax.cnt.push_back(i1 - i0 + 1);
+                    }
+                    return ax;
+                };
+                /* pick the grid minimising the expected records per lookup (uniform hit points over
+                   the plane's box), with at most max(16, 16 x records) cells; ties -> fewer cells */
+                const int k = (int)R.size(), cap = std::max(16, 16 * k), mmax = std::min(128, cap);
+                std::vector<Axis> us, vs;
+                for (int m = 1; m <= mmax; m++)
+                    for (int h = 0; h < 2; h++) {
+                        us.push_back(make_axis(ulo, eu, m, h, true));
+                        vs.push_back(make_axis(vlo, ev, m, h, false));
+                    }
+                double best_cost = 1e300;
+                size_t bu = 0, bv = 0;
+                for (size_t x = 0; x < us.size(); x++)
+                    for (size_t y = 0; y < vs.size(); y++) {
+                        const double cells = (double)us[x].n * vs[y].n;
+                        if (cells > cap) continue;
+                        double sum = 0;
+                        for (int i = 0; i < k; i++) sum += (double)us[x].cnt[i] * vs[y].cnt[i];
+                        const double cost = sum / cells + 1e-6 * cells;
+                        if (cost < best_cost) {
+                            best_cost = cost;
+                            bu = x;
+                            bv = y;
+                        }
+                    }
+                const Axis &AU = us[bu], &AV = vs[bv];
+                const int nu = AU.n, nv = AV.n;
+                GridPlane g;
+                memset(&g, 0, sizeof g);
+                g.plane = pk;
+                g.u0 = AU.o;
+                g.v0 = AV.o;
+                g.iu = AU.inv;
+                g.iv = AV.inv;
+                g.nu = nu;
+                g.nv = nv;
+                g.cell_off = (int32_t)(gb.cells.size() / 2);
+                const double su = AU.slack, sv = AV.slack;
+                std::vector<std::vector<const FilterRec *>> bucket((size_t)nu * nv);
+                for (const FilterRec *r : R) {
+                    int u0, u1, v0, v1;
+                    lo_hi(r->cu, r->hwu, g.u0, g.iu, su, nu, u0, u1);
+                    lo_hi(r->cv, r->hwv, g.v0, g.iv, sv, nv, v0, v1);
+                    for (int iv = v0; iv <= v1; iv++)
+                        for (int iu = u0; iu <= u1; iu++) bucket[(size_t)iv * nu + iu].push_back(r);
+                }
+                for (const auto &b : bucket) {
+                    gb.cells.push_back((uint32_t)gb.idx.size());
+                    gb.cells.push_back((uint32_t)b.size());
+                    for (const FilterRec *r : b) {
+                        gb.recs.insert(gb.recs.end(), {r->cu, r->hwu, r->cv, r->hwv});
+                        gb.idx.push_back(r->idx);
+                    }
+                }
+                planes[a][c].push_back(g);
+            }
+        }
+    }
+    GridPlane pad;
+    memset(&pad, 0, sizeof pad);
+    pad.plane = NAN; /* fac' = NaN: never a candidate */
+    pad.nu = pad.nv = 1;
+    pad.cell_off = 0;
+    for (int a = 0; a < 3; a++) {
+        gb.J[a] = (int)std::max(planes[a][0].size(), planes[a][1].size());
+        for (int j = 0; j < gb.J[a]; j++)
+            for (int c = 0; c < 2; c++) gb.img.push_back(j < (int)planes[a][c].size() ? planes[a][c][j] : pad);
+    }
+    if (gb.img.empty()) gb.img.push_back(pad);
+    if (gb.idx.empty()) { /* keep the device arrays non-empty */
+        gb.recs.insert(gb.recs.end(), {0.f, -1.f, 0.f, -1.f});
+        gb.idx.push_back(-1);
+    }
+    return gb;
 }
 
 /* Exact deposit colour of every colour state (kernel: k_bake's `sid`), in fixed point. The float ops
@@ -241,6 +396,15 @@ struct fmgi_context {
     int fimg_bytes = 0;
     int32_t *d_general = nullptr;
     int fJ[3] = {0, 0, 0};
+    /* ScanGrid tables */
+    GridPlane *d_gimg = nullptr;
+    int gimg_bytes = 0;
+    int gJ[3] = {0, 0, 0};
+    uint32_t *d_gcells = nullptr;
+    float *d_grecs = nullptr;
+    int32_t *d_gidx = nullptr;
+    int grid_cells = 0, grid_entries = 0;
+    GridBuild h_grid; /* host copy (fmgi_grid_copy) */
     int ngeneral = 0;
     float margin = 0;
     /* accumulation: FMGI_ACCUM_FX3 or FMGI_ACCUM_STATE (counts[1024][numTexels] + colour table) */
@@ -315,6 +479,10 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_launches);
     hipFree(c->d_fimg);
     hipFree(c->d_general);
+    hipFree(c->d_gimg);
+    hipFree(c->d_gcells);
+    hipFree(c->d_grecs);
+    hipFree(c->d_gidx);
     hipFree(c->d_src_item_begin);
     hipFree(c->d_src_launch0);
     hipFree(c->d_counts);
@@ -439,6 +607,12 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->fimg_bytes = (int)(fb.img.size() * sizeof(FilterRec));
     c->ngeneral = (int)fb.general.size();
     c->margin = fb.margin;
+    GridBuild gb = build_grid(fb);
+    for (int a = 0; a < 3; a++) c->gJ[a] = gb.J[a];
+    c->gimg_bytes = (int)(gb.img.size() * sizeof(GridPlane));
+    c->grid_cells = (int)(gb.cells.size() / 2);
+    c->grid_entries = (int)gb.idx.size();
+    c->h_grid = gb;
     if (c->device != FMGI_HOST_ONLY) {
     HIPCHK(hipSetDevice(c->device));
     hipFree(c->d_rects);
@@ -463,6 +637,18 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
         HIPCHK(hipMalloc(&c->d_general, fb.general.size() * sizeof(int32_t)));
         HIPCHK(hipMemcpy(c->d_general, fb.general.data(), fb.general.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     }
+    hipFree(c->d_gimg);
+    hipFree(c->d_gcells);
+    hipFree(c->d_grecs);
+    hipFree(c->d_gidx);
+    c->d_gimg = nullptr;
+    c->d_gcells = nullptr;
+    c->d_grecs = nullptr;
+    c->d_gidx = nullptr;
+    HIPCHK(upload(&c->d_gimg, gb.img));
+    HIPCHK(upload(&c->d_gcells, gb.cells));
+    HIPCHK(upload(&c->d_grecs, gb.recs));
+    HIPCHK(upload(&c->d_gidx, gb.idx));
     }
     c->num_texels = num_texels;
     if (c->device != FMGI_HOST_ONLY) {
@@ -563,11 +749,15 @@ FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
     return n;
 }
 
+static int lds_bytes(const fmgi_context *c, int kernel) {
+    return kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : c->fimg_bytes;
+}
+
 static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, uint64_t items) {
     /* persistent grid: exactly the blocks that are resident at once (occupancy from the VGPR/SGPR/LDS
        use of the kernel actually launched), so no block starts late and lengthens the tail; never more
        lanes than work items */
-    int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, c->fimg_bytes);
+    int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, lds_bytes(c, kernel));
     if (per_cu <= 0) per_cu = 4;
     uint64_t lanes_max = (uint64_t)c->num_cus * per_cu * block;
     uint64_t lanes = std::min<uint64_t>(items, lanes_max);
@@ -581,6 +771,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (e > c->total_items || b > e) return set_err(FMGI_ERR_ARG, "item range [%llu,%llu) outside plan of %llu items",
                                                   (unsigned long long)b, (unsigned long long)e,
                                                   (unsigned long long)c->total_items);
+    if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_GRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     if (b == e) return FMGI_OK;
     if (c->nrects == 0 || c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     HIPCHK(hipSetDevice(c->device));
@@ -601,9 +792,18 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.counter = c->d_counter;
     a.lm = (unsigned long long *)lm;
     a.stats = c->d_stats;
-    a.fimg = c->d_fimg;
-    a.fimg_bytes = c->fimg_bytes;
-    for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
+    if (kernel == FMGI_KERNEL_GRID) {
+        a.fimg = c->d_gimg;
+        a.fimg_bytes = c->gimg_bytes;
+        for (int k = 0; k < 3; k++) a.fJ[k] = c->gJ[k];
+        a.gcells = c->d_gcells;
+        a.grecs = c->d_grecs;
+        a.gridx = c->d_gidx;
+    } else {
+        a.fimg = c->d_fimg;
+        a.fimg_bytes = c->fimg_bytes;
+        for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
+    }
     a.general = c->d_general;
     a.ngeneral = c->ngeneral;
     a.counts = c->accum == FMGI_ACCUM_STATE ? c->d_counts : nullptr;
@@ -656,6 +856,24 @@ FMGI_API int fmgi_finalize(fmgi_context *c, const void *lm, const void *tin, voi
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(fmgi_launch_finalize((const unsigned long long *)lm, (const float *)tin, (float *)tout, c->num_texels,
                                 stream ? (hipStream_t)stream : c->stream));
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_grid_sizes(const fmgi_context *c, int32_t sizes[5]) {
+    if (!c || !sizes) return set_err(FMGI_ERR_ARG, "fmgi_grid_sizes: bad arguments");
+    for (int a = 0; a < 3; a++) sizes[a] = c->h_grid.J[a];
+    sizes[3] = (int32_t)(c->h_grid.cells.size() / 2);
+    sizes[4] = (int32_t)c->h_grid.idx.size();
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_grid_copy(const fmgi_context *c, void *planes, uint32_t *cells, float *recs, int32_t *idx) {
+    if (!c) return set_err(FMGI_ERR_ARG, "fmgi_grid_copy: null context");
+    const GridBuild &g = c->h_grid;
+    if (planes) memcpy(planes, g.img.data(), g.img.size() * sizeof(GridPlane));
+    if (cells) memcpy(cells, g.cells.data(), g.cells.size() * sizeof(uint32_t));
+    if (recs) memcpy(recs, g.recs.data(), g.recs.size() * sizeof(float));
+    if (idx) memcpy(idx, g.idx.data(), g.idx.size() * sizeof(int32_t));
     return FMGI_OK;
 }
 
@@ -756,7 +974,9 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     int wg = wg_env ? atoi(wg_env) : 256;
     if (wg <= 0) wg = 256;
     const char *k_env = getenv("FMGI_KERNEL");
-    int kernel = (k_env && !strcmp(k_env, "exact")) ? FMGI_KERNEL_EXACT : FMGI_KERNEL_FAST;
+    int kernel = FMGI_KERNEL_GRID;
+    if (k_env && !strcmp(k_env, "exact")) kernel = FMGI_KERNEL_EXACT;
+    if (k_env && !strcmp(k_env, "fast")) kernel = FMGI_KERNEL_FAST;
     int ndev = fmgi_device_count();
     if (ndev <= 0) return set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
     const char *g_env = getenv("FMGI_GPUS");

@@ -20,6 +20,16 @@ struct FilterRec {
 };
 static_assert(sizeof(FilterRec) == 32, "FilterRec must be 32 B");
 
+/* One plane of the grid kernel (ScanGrid): all axis-aligned rects of one class (axis a, normal sign)
+   that lie in the plane x_a = plane, bucketed by a nu x nv grid over the plane's (u, v) bounding box of
+   their margin-grown extents. Cell (iu, iv) = cells[cell_off + iv*nu + iu] = {first record, count}. */
+struct GridPlane {
+    float plane, u0, v0, iu; /* iu, iv = cells per unit length */
+    float iv;
+    int32_t nu, nv, cell_off;
+};
+static_assert(sizeof(GridPlane) == 32, "GridPlane must be 32 B");
+
 struct BakeArgs {
     const RectDev *rects;
     int nrects;
@@ -43,6 +53,12 @@ struct BakeArgs {
     int fJ[3];
     const int32_t *general;
     int ngeneral;
+    /* grid kernel (ScanGrid): fimg/fJ then hold GridPlane pairs {+a plane j, -a plane j}; the cells
+       ({start, count} u32 pairs), the per-cell records (float4 {cu, hwu, cv, hwv}) and their rect
+       indices live in global memory */
+    const uint32_t *gcells;
+    const float *grecs;
+    const int32_t *gridx;
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
     unsigned long long *counts;
     /* AccStream accumulation: deposit codes (texel << 10 | colour state) appended to stream[0..cap) in

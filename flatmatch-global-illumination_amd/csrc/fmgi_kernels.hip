@@ -198,6 +198,154 @@ struct ScanFast {
     }
 };
 
+/*
+ * ScanGrid: ScanFast's phase 1 with the rects of each plane bucketed by a 2-D grid.
+ *
+ * Rects of one class that share a plane share phase 1's fac' = (plane - src_a) * rcp(dir_a) and hit
+ * point, so a lane evaluates fac' once per facing plane and tests only the records of the grid cell the
+ * hit point falls in. Every rect whose margin-grown extent contains the hit point is registered in that
+ * cell (the host registers each rect in every cell its grown extent overlaps, widened by a cell-rounding
+ * slack), so the candidate set still contains V and the keys are ScanFast's bit for bit: phase 2 and
+ * its separation argument carry over unchanged. A closed box of 200 rects has 6 planes: ~3 cells and a
+ * few records per scan instead of ~100 rect tests.
+ */
+template <int A>
+__device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, int J, f3 s, f3 d, float &L1,
+                                          float &L2, int &code1, unsigned &ntest) {
+    constexpr int U = (A == 0) ? 1 : 0;
+    constexpr int V = (A == 2) ? 1 : 2;
+    const float sa = comp<A>(s), da = comp<A>(d);
+    const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
+    const float rd = __builtin_amdgcn_rcpf(da);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 32), 16);
+    const uint2 *cells = (const uint2 *)a.gcells;
+    const float4 *recs = (const float4 *)a.grecs;
+    for (int j = 0; j < J; j++) {
+        const float4 q0 = p[4 * j];     /* plane, u0, v0, iu */
+        const float4 q1 = p[4 * j + 1]; /* iv, nu, nv, cell_off */
+        const float f = (q0.x - sa) * rd;
+        if (!(f >= 0.0f)) continue; /* plane behind the photon (or NaN): no candidate on it */
+        const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
+        const int nu = __float_as_int(q1.y), nv = __float_as_int(q1.z), off = __float_as_int(q1.w);
+        const float tu = fminf(fmaxf((uh - q0.y) * q0.w, 0.0f), (float)(nu - 1));
+        const float tv = fminf(fmaxf((vh - q0.z) * q1.x, 0.0f), (float)(nv - 1));
+        const uint2 c = cells[off + (int)tv * nu + (int)tu];
+        ntest += c.y;
+        for (uint32_t k = 0; k < c.y; k++) {
+            const float4 r = recs[c.x + k];
+            const bool ok = (int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w);
+            const float key = ok ? f : INFINITY;
+            const bool lt = key < L1;
+            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+            code1 = lt ? (int)(c.x + k) : code1;
+            L1 = lt ? key : L1;
+        }
+    }
+}
+
+/* calls fn(idx) for the rect index of every record that passes grid_axis's candidate test */
+template <int A, class F>
+__device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, int J, f3 s, f3 d, F &&fn) {
+    constexpr int U = (A == 0) ? 1 : 0;
+    constexpr int V = (A == 2) ? 1 : 2;
+    const float sa = comp<A>(s), da = comp<A>(d);
+    const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
+    const float rd = __builtin_amdgcn_rcpf(da);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 32), 16);
+    const uint2 *cells = (const uint2 *)a.gcells;
+    const float4 *recs = (const float4 *)a.grecs;
+    for (int j = 0; j < J; j++) {
+        const float4 q0 = p[4 * j];
+        const float4 q1 = p[4 * j + 1];
+        const float f = (q0.x - sa) * rd;
+        if (!(f >= 0.0f)) continue;
+        const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
+        const int nu = __float_as_int(q1.y), nv = __float_as_int(q1.z), off = __float_as_int(q1.w);
+        const float tu = fminf(fmaxf((uh - q0.y) * q0.w, 0.0f), (float)(nu - 1));
+        const float tv = fminf(fmaxf((vh - q0.z) * q1.x, 0.0f), (float)(nv - 1));
+        const uint2 c = cells[off + (int)tv * nu + (int)tu];
+        for (uint32_t k = 0; k < c.y; k++) {
+            const float4 r = recs[c.x + k];
+            if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[c.x + k]);
+        }
+    }
+}
+
+struct ScanGrid {
+    static constexpr bool kLds = true;
+    static constexpr int kOrderedRounds = 12;
+
+    /*
+     * The literal scan (photonmap.cl:189-206) restricted to the phase-1 candidates, in rect-index order.
+     * A rect outside V returns -1 from intersects() whatever `closest` is, so skipping it cannot change
+     * the result; the candidates are a superset of V, so this equals ScanExact. Each round finds the next
+     * candidate index by re-walking the cells (typically 2-3 candidates: a tie on a shared edge).
+     */
+    static __device__ int ordered_exact(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best) {
+        cptr<RectDev> R = (cptr<RectDev>)a.rects;
+        int prev = -1, hit = -1;
+        float closest = INFINITY;
+        for (int round = 0; round < kOrderedRounds; round++) {
+            int nxt = INT_MAX;
+            auto take = [&](int idx) { nxt = (idx > prev && idx < nxt) ? idx : nxt; };
+            grid_visit<0>(a, lds, a.fJ[0], src, dir, take);
+            grid_visit<1>(a, lds + 64 * a.fJ[0], a.fJ[1], src, dir, take);
+            grid_visit<2>(a, lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
+            for (int g = 0; g < a.ngeneral; g++) {
+                const int idx = a.general[g];
+                if (idx > prev && idx < nxt && exact_on(R, idx, src, dir, INFINITY) >= 0) nxt = idx;
+            }
+            if (nxt == INT_MAX) {
+                best = closest;
+                return hit;
+            }
+            const float d = exact_on(R, nxt, src, dir, closest);
+            if (d >= 0 && d < closest) {
+                closest = d;
+                hit = nxt;
+            }
+            prev = nxt;
+        }
+        return -2; /* more candidates than rounds: caller runs the full literal scan */
+    }
+
+    static __device__ __forceinline__ int scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best,
+                                               ScanStats &st) {
+        float L1 = INFINITY, L2 = INFINITY;
+        int code1 = -1;
+        unsigned ntest = 0;
+        grid_axis<0>(a, lds, a.fJ[0], src, dir, L1, L2, code1, ntest);
+        grid_axis<1>(a, lds + 64 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
+        grid_axis<2>(a, lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
+        cptr<RectDev> R = (cptr<RectDev>)a.rects;
+        cptr<int32_t> G = (cptr<int32_t>)a.general;
+        for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
+            const float f = exact_on(R, G[g], src, dir, INFINITY);
+            const float key = (f < 0) ? INFINITY : f;
+            const bool lt = key < L1;
+            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+            code1 = lt ? -2 - g : code1;
+            L1 = lt ? key : L1;
+        }
+        st.tests += (unsigned long long)(ntest + (unsigned)a.ngeneral);
+        if (L1 == INFINITY) {
+            best = INFINITY;
+            return -1;
+        }
+        const int idx = code1 >= 0 ? a.gridx[code1] : a.general[-2 - code1];
+        const float f = exact_at(a.rects[idx], src, dir, INFINITY);
+        if (!(f < 0) && L2 > f * 1.000244140625f) { /* ScanFast's separation test */
+            best = f;
+            return idx;
+        }
+        st.rescans++;
+        if (f < 0) st.invalid++; else st.ties++;
+        const int r = ordered_exact(a, lds, src, dir, best);
+        if (r != -2) return r;
+        return ScanExact::scan(a, lds, src, dir, best, st);
+    }
+};
+
 /* ---- accumulation policies -------------------------------------------------------------------- */
 
 /* three exact int64 fixed-point atomics per deposit into lm[texel][0..2] */
@@ -525,6 +673,12 @@ const void *kernel_ptr(bool trace) {
 }
 
 const void *bake_kernel(int kernel, int accum, bool trace) {
+    if (kernel == 2) {
+        if (accum == 2) return kernel_ptr<ScanGrid, AccState>(trace);
+        if (accum == 3) return kernel_ptr<ScanGrid, AccNone>(trace);
+        if (accum == 4) return kernel_ptr<ScanGrid, AccStream>(trace);
+        return kernel_ptr<ScanGrid, AccFx3>(trace);
+    }
     if (kernel == 1) {
         if (accum == 2) return kernel_ptr<ScanFast, AccState>(trace);
         if (accum == 3) return kernel_ptr<ScanFast, AccNone>(trace);
@@ -542,7 +696,7 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bake_kernel(kernel, accum, trace), block,
-                                                     kernel == 1 ? (size_t)lds_bytes : 0) != hipSuccess)
+                                                     kernel != 0 ? (size_t)lds_bytes : 0) != hipSuccess)
         return 0;
     return n;
 }
@@ -550,8 +704,13 @@ int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int 
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s) {
     dim3 grid(grid_blocks), blk(block);
-    const size_t lds = kernel == 1 ? (size_t)a.fimg_bytes : 0;
-    if (kernel == 1) { /* FMGI_KERNEL_FAST */
+    const size_t lds = kernel != 0 ? (size_t)a.fimg_bytes : 0;
+    if (kernel == 2) { /* FMGI_KERNEL_GRID */
+        if (accum == 2) launch3<ScanGrid, AccState>(a, trace, grid, blk, lds, s);
+        else if (accum == 3) launch3<ScanGrid, AccNone>(a, trace, grid, blk, lds, s);
+        else if (accum == 4) launch3<ScanGrid, AccStream>(a, trace, grid, blk, lds, s);
+        else launch3<ScanGrid, AccFx3>(a, trace, grid, blk, lds, s);
+    } else if (kernel == 1) { /* FMGI_KERNEL_FAST */
         if (accum == 2) launch3<ScanFast, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanFast, AccNone>(a, trace, grid, blk, lds, s);
         else if (accum == 4) launch3<ScanFast, AccStream>(a, trace, grid, blk, lds, s);

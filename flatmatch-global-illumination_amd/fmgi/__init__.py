@@ -18,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import scene
-from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_EXACT, KERNEL_FAST, FmgiError, Geometry, Stats,
+from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, FmgiError, Geometry, Stats,
                    check, load)
 from .scene import RECT_DTYPE, Scene
 
@@ -42,6 +42,7 @@ __all__ = [
     "FmgiError",
     "KERNEL_EXACT",
     "KERNEL_FAST",
+    "KERNEL_GRID",
     "ACCUM_AUTO",
     "ACCUM_FX3",
     "ACCUM_STATE",
@@ -141,7 +142,7 @@ class Context:
         check(self.lib.fmgi_get_plan(self.h, _ptr(out), len(out)), "fmgi_get_plan")
         return out
 
-    def bake_items(self, begin: int, end: int, lm_fx_ptr: int, kernel: int = KERNEL_FAST, stream: int = 0):
+    def bake_items(self, begin: int, end: int, lm_fx_ptr: int, kernel: int = KERNEL_GRID, stream: int = 0):
         """Launch on `stream` (a hipStream_t as int; pass the stream that produced lm_fx). 0/None selects
         the context's internal stream, which is NOT ordered with torch's default stream."""
         check(self.lib.fmgi_bake_items(self.h, begin, end, C.c_void_p(lm_fx_ptr), kernel, C.c_void_p(stream or None)),
@@ -162,7 +163,7 @@ class Context:
     def reset_stats(self):
         check(self.lib.fmgi_reset_stats(self.h), "fmgi_reset_stats")
 
-    def trace_items(self, begin: int, end: int, kernel: int = KERNEL_FAST):
+    def trace_items(self, begin: int, end: int, kernel: int = KERNEL_GRID):
         """Per-photon bounce records of items [begin, end): (events[n, 800], counts[n], rng_final[n])."""
         n = end - begin
         ev = np.zeros(n * EVENTS_PER_ITEM, EVENT_DTYPE)
@@ -171,12 +172,30 @@ class Context:
         check(self.lib.fmgi_trace_items(self.h, begin, end, kernel, _ptr(ev), _ptr(cnt), _ptr(rng)), "fmgi_trace_items")
         return ev.reshape(n, EVENTS_PER_ITEM), cnt, rng
 
+    def grid_tables(self) -> dict:
+        """FMGI_KERNEL_GRID's plane/cell/record tables (include/flatmatch_gi.h fmgi_grid_copy)."""
+        sz = np.zeros(5, np.int32)
+        check(self.lib.fmgi_grid_sizes(self.h, _ptr(sz)), "fmgi_grid_sizes")
+        npairs = int(sz[:3].sum())
+        planes = np.zeros(2 * max(npairs, 1), GRID_PLANE_DTYPE)
+        cells = np.zeros((int(sz[3]), 2), np.uint32)
+        recs = np.zeros((int(sz[4]), 4), np.float32)
+        idx = np.zeros(int(sz[4]), np.int32)
+        check(self.lib.fmgi_grid_copy(self.h, _ptr(planes), _ptr(cells), _ptr(recs), _ptr(idx)), "fmgi_grid_copy")
+        return {"J": [int(x) for x in sz[:3]], "planes": planes[: 2 * npairs], "cells": cells, "recs": recs,
+                "idx": idx}
+
     def device_sincosf(self, x: np.ndarray):
         x = np.ascontiguousarray(x, np.float32)
         s = np.empty_like(x)
         c = np.empty_like(x)
         check(self.lib.fmgi_device_sincosf(self.h, _ptr(x), _ptr(s), _ptr(c), len(x)), "fmgi_device_sincosf")
         return s, c
+
+
+GRID_PLANE_DTYPE = np.dtype([("plane", "<f4"), ("u0", "<f4"), ("v0", "<f4"), ("iu", "<f4"), ("iv", "<f4"),
+                             ("nu", "<i4"), ("nv", "<i4"), ("cell_off", "<i4")])
+assert GRID_PLANE_DTYPE.itemsize == 32
 
 
 def make_geometry(sc: Scene, texels: np.ndarray):

@@ -31,10 +31,13 @@ EXPORTS = (
     "fmgi_trace_items",
     "fmgi_host_sincosf",
     "fmgi_device_sincosf",
+    "fmgi_grid_sizes",
+    "fmgi_grid_copy",
 )
 
 KERNEL_EXACT = 0
 KERNEL_FAST = 1
+KERNEL_GRID = 2
 ACCUM_AUTO = 0
 ACCUM_FX3 = 1
 ACCUM_STATE = 2
@@ -117,6 +120,8 @@ def load() -> C.CDLL:
         "fmgi_trace_items": (C.c_int, [vp, u64, u64, C.c_int, vp, vp, vp]),
         "fmgi_host_sincosf": (None, [vp, vp, vp, i64]),
         "fmgi_device_sincosf": (C.c_int, [vp, vp, vp, vp, i64]),
+        "fmgi_grid_sizes": (C.c_int, [vp, vp]),
+        "fmgi_grid_copy": (C.c_int, [vp, vp, vp, vp, vp]),
         "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
         "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),
     }

@@ -21,7 +21,7 @@
  *   FMGI_WG        virtual OpenCL work-group size of the launch schedule (default 256, the value
  *                  ROCm's OpenCL reports for CL_KERNEL_WORK_GROUP_SIZE; global_illumination_cl.c:300)
  *   FMGI_GPUS      number of GPUs to shard over (default: all visible, max 8)
- *   FMGI_KERNEL    "fast" (default) or "exact" -- both produce identical bits; see DESIGN.md
+ *   FMGI_KERNEL    "grid" (default), "fast" or "exact" -- all produce identical bits; see DESIGN.md
  *   FMGI_QUIET     1 = suppress the reference's progress line
  */
 #ifndef FLATMATCH_GI_H
@@ -72,7 +72,9 @@ enum {
     FMGI_ERR_OOM = -5
 };
 
-enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1 };
+/* Scan kernels (identical bits): EXACT = photonmap.cl's scan over every rect; FAST = conservative fp32
+   filter over every rect + exact verification; GRID = FAST's filter over per-plane grid cells only. */
+enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2 };
 /* Deposit accumulation (both exact and order-free; results are identical):
    FX3   three int64 fixed-point atomics per deposit into the lightmap;
    STATE one u64 atomic per deposit into counts[colour state][texel] (8 KiB per texel of device memory),
@@ -166,6 +168,16 @@ int fmgi_reset_stats(fmgi_context *ctx);
    of events per item in counts[], and the final per-item RNG state in rng_final[]. Synchronous. */
 int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, int kernel,
                      fmgi_event *events, int32_t *counts, uint32_t *rng_final);
+
+/* Grid tables of FMGI_KERNEL_GRID (built by fmgi_set_scene; host-only contexts too), for tests and
+   tooling. sizes[0..2] = plane pairs per axis (x, y, z), sizes[3] = cells, sizes[4] = cell entries.
+   fmgi_grid_copy fills (any pointer may be NULL):
+     planes[2 * (sizes[0] + sizes[1] + sizes[2])]: per axis, pairs {plane of the +n class, plane of the
+       -n class}, each {float plane, u0, v0, iu, iv; int32 nu, nv, cell_off} (32 B; NaN plane = padding);
+     cells[2 * sizes[3]]: {first entry, count}; recs[4 * sizes[4]]: {cu, hwu, cv, hwv} (margin-grown
+     extents); idx[sizes[4]]: rect index. */
+int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);
+int fmgi_grid_copy(const fmgi_context *ctx, void *planes, uint32_t *cells, float *recs, int32_t *idx);
 
 /* Host helpers exported for tests (no device needed). */
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);

@@ -17,7 +17,7 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = [fmgi.KERNEL_EXACT, fmgi.KERNEL_FAST]
+KERNELS = [fmgi.KERNEL_EXACT, fmgi.KERNEL_FAST, fmgi.KERNEL_GRID]
 
 
 @pytest.fixture(scope="module")
@@ -152,22 +152,22 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     spa = 172_413_793
     ctx = _ctx(box200, spa, offsets, fmgi.ACCUM_STATE)
     n = ctx.total_items  # BASELINE config 3 at full size: 1,000,012,800 photons
-    a = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
-    b1 = _bake_gpu(torch_cuda, ctx, 0, n // 3, fmgi.KERNEL_FAST)
-    b2 = _bake_gpu(torch_cuda, ctx, n // 3, n, fmgi.KERNEL_FAST)
+    a = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+    b1 = _bake_gpu(torch_cuda, ctx, 0, n // 3, fmgi.KERNEL_GRID)
+    b2 = _bake_gpu(torch_cuda, ctx, n // 3, n, fmgi.KERNEL_GRID)
     ctx.set_accumulation(fmgi.ACCUM_FX3)
-    c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
+    c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
     ctx.set_accumulation(fmgi.ACCUM_STREAM)
-    d = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)  # 3 chunks of <= 4e6 items
-    d1 = _bake_gpu(torch_cuda, ctx, 0, 12_345, fmgi.KERNEL_FAST)
-    d2 = _bake_gpu(torch_cuda, ctx, 12_345, n, fmgi.KERNEL_FAST)
+    d = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)  # 3 chunks of <= 4e6 items
+    d1 = _bake_gpu(torch_cuda, ctx, 0, 12_345, fmgi.KERNEL_GRID)
+    d2 = _bake_gpu(torch_cuda, ctx, 12_345, n, fmgi.KERNEL_GRID)
     assert np.array_equal(a, b1 + b2)
     assert np.array_equal(a, c)  # the accumulation modes agree bit for bit
     assert np.array_equal(a, d)
     assert np.array_equal(a, d1 + d2)
     assert ctx.stats()["stream_overflow"] == 0
     ctx.reset_stats()
-    _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_FAST)
+    _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
     st = ctx.stats()
     assert st["photons"] == 100 * n
     assert st["deposits"] + st["escapes"] == st["scans"]

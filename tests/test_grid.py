@@ -1,0 +1,107 @@
+"""CPU tests of FMGI_KERNEL_GRID's tables (host-only context; no device needed).
+
+ScanGrid (csrc/fmgi_kernels.hip) is exact only if, for every hit point (u, v) on a plane, the grid
+cell the kernel computes for (u, v) lists EVERY record of that plane whose margin-grown extent
+contains (u, v) -- the candidate set must stay a superset of photonmap.cl's valid set V. Here the
+kernel's cell arithmetic is replayed in float32 (IEEE, same operation order) on random points and on
+adversarial points at every record's extent boundaries (and one ulp either side)."""
+import numpy as np
+import pytest
+
+import fmgi
+
+
+def _tables(sc):
+    ctx = fmgi.Context(-1)
+    ctx.set_scene(sc)
+    t = ctx.grid_tables()
+    ctx.close()
+    return t
+
+
+def _planes(t):
+    """(plane record, entries of every cell) for each non-padding plane."""
+    out = []
+    for p in t["planes"]:
+        if np.isnan(p["plane"]):
+            continue
+        n = int(p["nu"]) * int(p["nv"])
+        cells = t["cells"][p["cell_off"] : p["cell_off"] + n]
+        out.append((p, cells))
+    return out
+
+
+def _cell_of(p, u, v):
+    """The kernel's cell index for hit point (u, v): fminf(fmaxf((x - o) * inv, 0), n - 1), truncated."""
+    f32 = np.float32
+    tu = np.minimum(np.maximum((u - f32(p["u0"])) * f32(p["iu"]), f32(0)), f32(p["nu"] - 1))
+    tv = np.minimum(np.maximum((v - f32(p["v0"])) * f32(p["iv"]), f32(0)), f32(p["nv"] - 1))
+    return tv.astype(np.int64) * int(p["nu"]) + tu.astype(np.int64)
+
+
+def _check_plane(t, p, cells, rng):
+    ent = np.unique(np.concatenate([np.arange(s, s + c) for s, c in cells if c] or [np.zeros(0, np.int64)]))
+    recs = t["recs"][ent]
+    ids = t["idx"][ent]
+    # one record per rect of this plane (a rect's entries all carry the same extent)
+    uniq, first = np.unique(ids, return_index=True)
+    recs, ids = recs[first], uniq
+    cu, hwu, cv, hwv = (recs[:, k].astype(np.float32) for k in range(4))
+    # candidate points: extent corners/edges +- 1 ulp, centres, and uniform random points
+    us, vs = [], []
+    for du in (-hwu, hwu):
+        for sgn in (-1, 0, 1):
+            u = (cu + du).astype(np.float32)
+            u = np.nextafter(u, np.float32(np.inf) if sgn > 0 else np.float32(-np.inf)) if sgn else u
+            for v in ((cv - hwv).astype(np.float32), cv, (cv + hwv).astype(np.float32)):
+                us.append(u)
+                vs.append(v)
+    for dv in (-hwv, hwv):
+        for sgn in (-1, 0, 1):
+            v = (cv + dv).astype(np.float32)
+            v = np.nextafter(v, np.float32(np.inf) if sgn > 0 else np.float32(-np.inf)) if sgn else v
+            us.append(cu)
+            vs.append(v)
+    lo_u, hi_u = float((cu - hwu).min()), float((cu + hwu).max())
+    lo_v, hi_v = float((cv - hwv).min()), float((cv + hwv).max())
+    us.append(rng.uniform(lo_u, hi_u, 20000).astype(np.float32))
+    vs.append(rng.uniform(lo_v, hi_v, 20000).astype(np.float32))
+    U = np.concatenate(us)
+    V = np.concatenate(vs)
+    cell = _cell_of(p, U, V)
+    # every record containing the point must be listed in the point's cell
+    inside = (np.abs(U[:, None] - cu[None, :]) <= hwu[None, :]) & (np.abs(V[:, None] - cv[None, :]) <= hwv[None, :])
+    lists = [set(t["idx"][s : s + c].tolist()) for s, c in cells]
+    missing = 0
+    for k in np.nonzero(inside.any(axis=1))[0]:
+        need = set(ids[inside[k]].tolist())
+        if not need <= lists[cell[k]]:
+            missing += 1
+    assert missing == 0, f"{missing} points whose containing records are not in their cell"
+    return len(ids)
+
+
+@pytest.mark.parametrize("name", ["example", "box200", "box2000", "box8"])
+def test_grid_cells_cover_every_containing_record(name, example_scene, box200, box2000):
+    from fmgi import scene
+
+    sc = {"example": example_scene, "box200": box200, "box2000": box2000, "box8": scene.box_scene(8)}[name]
+    t = _tables(sc)
+    rng = np.random.default_rng(7)
+    n = 0
+    for p, cells in _planes(t):
+        n += _check_plane(t, p, cells, rng)
+    # every rect of these scenes is axis-aligned, so every rect is on exactly one grid plane
+    assert n == len(sc.walls)
+
+
+def test_grid_is_small_and_selective(box200, box2000):
+    """Expected records per lookup stays near 1 on the synthetic boxes (the point of the grid)."""
+    for sc in (box200, box2000):
+        t = _tables(sc)
+        planes = _planes(t)
+        assert len(planes) == 6  # a closed box: six planes
+        tot = sum(len(c) for _, c in planes)
+        ent = sum(int(c[:, 1].sum()) for _, c in planes)
+        assert tot <= 16 * len(sc.walls) + 16 * 6
+        assert ent / tot < 2.0, ent / tot
