@@ -91,7 +91,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", default="grid", choices=["grid", "fast", "exact"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "grid", "fast", "exact"])
     ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state", "stream", "none"],
                     help="none = PROFILING ONLY (deposits discarded; lightmap wrong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -121,7 +121,8 @@ def main():
     sc = load_scene(cfg["scene"])
     spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
     spa = min(spa, 2**31 - 1)
-    kernel = {"grid": fmgi.KERNEL_GRID, "fast": fmgi.KERNEL_FAST, "exact": fmgi.KERNEL_EXACT}[args.kernel]
+    kernel = {"auto": fmgi.KERNEL_AUTO, "grid": fmgi.KERNEL_GRID, "fast": fmgi.KERNEL_FAST,
+              "exact": fmgi.KERNEL_EXACT}[args.kernel]
 
     ctx = fmgi.Context(local)
     ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE,
@@ -159,9 +160,11 @@ def main():
         if rank == 0:
             ctx.finalize(lm.data_ptr(), tex_in.data_ptr(), tex_out.data_ptr(), sptr)
 
+    ctx.set_timing(True)  # HIP events around every k_bake / fold launch, on the bake's stream
     for _ in range(args.warmup):
         step(False)
     torch.cuda.synchronize()
+    ctx.timing()  # drop the warm-up launches
     ctx.reset_stats()
     if world > 1:
         dist.barrier()
@@ -174,7 +177,10 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
-    kernel_ms = float(np.mean([s.elapsed_time(x) for s, x in k_ms]))
+    span_ms = float(np.mean([s.elapsed_time(x) for s, x in k_ms]))  # whole fmgi_bake_items per step
+    tim = ctx.timing()
+    bake_launch_ms = tim["bake_ms"] / max(tim["bake_launches"], 1)  # the dominant kernel, per launch
+    bake_launches = tim["bake_launches"]
 
     vals = torch.tensor([elapsed, st["scans"], st["deposits"], st["photons"]], dtype=torch.float64, device=dev)
     if world > 1:
@@ -190,12 +196,13 @@ def main():
     if rank == 0:
         assert int(photons_done) == photons_per_step * args.steps, (photons_done, photons_per_step)
         value = photons_per_step * args.steps / elapsed
-        # rank 0's dominant kernel (the bake) per launch: SURVEY.md §8d algorithmic work
-        per_launch_scans = st["scans"] / args.steps
-        per_launch_deps = st["deposits"] / args.steps
+        # rank 0's dominant kernel (k_bake) per launch: SURVEY.md §8d algorithmic work of the photons that
+        # launch traced (12 B per deposit; the 16 B/texel write-back belongs to fmgi_finalize)
+        per_launch_scans = st["scans"] / bake_launches
+        per_launch_deps = st["deposits"] / bake_launches
         flops = 40.0 * per_launch_scans * len(sc.walls) + 150.0 * per_launch_scans
-        hbm_bytes = 12.0 * per_launch_deps + 16.0 * sc.num_texels
-        ks = kernel_ms / 1e3
+        hbm_bytes = 12.0 * per_launch_deps
+        ks = bake_launch_ms / 1e3
         achieved_tf = flops / ks / 1e12
         achieved_gbs = hbm_bytes / ks / 1e9
         # memory-side atomic adds issued per second by the bake (1 per deposit for the colour-state
@@ -227,7 +234,8 @@ def main():
                 "texels": int(sc.num_texels),
                 "spa": spa,
                 "photons_per_step": photons_per_step,
-                "kernel": args.kernel,
+                "kernel": {0: "exact", 1: "fast", 2: "grid"}[kernel if kernel != fmgi.KERNEL_AUTO else ctx.auto_kernel]
+                + (" (auto)" if kernel == fmgi.KERNEL_AUTO else ""),
                 "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)",
                                  4: "stream"}[ctx.accumulation],
                 "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
@@ -241,7 +249,11 @@ def main():
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
                 "traffic": pmc_traffic(args.config),
-                "kernel_ms": kernel_ms,
+                "kernel": "k_bake",
+                "kernel_ms": bake_launch_ms,
+                "launches_per_step": bake_launches / args.steps,
+                "bake_path_ms_per_step": span_ms,
+                "fold_ms_per_step": tim["fold_ms"] / args.steps,
                 "algorithmic_bytes_per_launch": hbm_bytes,
                 "binding": binding,
                 "atomics": atomics,
@@ -261,6 +273,15 @@ def main():
                 "rescans_invalid_per_scan": st["rescans_invalid"] / max(st["scans"], 1),
             },
         }
+        if os.environ.get("FMGI_LIB") == "timing":  # profiling build: where the bake's wave time goes
+            import ctypes as C
+
+            cyc = (C.c_uint64 * 16)()
+            ctx.lib.fmgi_get_stage_cycles(ctx.h, cyc)
+            names = ["start", "sample", "scan_phase1", "scan_phase2", "fallback", "hit", "append"]
+            tot = sum(cyc[k] for k in range(len(names))) or 1
+            out["stage_cycles_frac"] = {n: cyc[k] / tot for k, n in enumerate(names)}
+            out["note"] = "PROFILING BUILD (s_memtime per stage): value is not a valid bench number"
         if world == 1 and not args.no_cpu_baseline:
             out["cpu_baseline"] = cpu_baseline(sc, cfg["spa"], args.cpu_seconds)
         print(json.dumps(out), flush=True)

@@ -306,6 +306,8 @@ GridBuild build_grid(const FilterBuild &fb) {
                 g.iv = AV.inv;
                 g.nu = nu;
                 g.nv = nv;
+                g.mu = (float)(nu - 1);
+                g.mv = (float)(nv - 1);
                 g.cell_off = (int32_t)(gb.cells.size() / 2);
                 const double su = AU.slack, sv = AV.slack;
                 std::vector<std::vector<const FilterRec *>> bucket((size_t)nu * nv);
@@ -332,6 +334,7 @@ GridBuild build_grid(const FilterBuild &fb) {
     memset(&pad, 0, sizeof pad);
     pad.plane = NAN; /* fac' = NaN: never a candidate */
     pad.nu = pad.nv = 1;
+    pad.mu = pad.mv = 0.0f;
     pad.cell_off = 0;
     for (int a = 0; a < 3; a++) {
         gb.J[a] = (int)std::max(planes[a][0].size(), planes[a][1].size());
@@ -405,6 +408,11 @@ struct fmgi_context {
     int32_t *d_gidx = nullptr;
     int grid_cells = 0, grid_entries = 0;
     GridBuild h_grid; /* host copy (fmgi_grid_copy) */
+    int auto_kernel = FMGI_KERNEL_FAST;
+    /* optional device timing (fmgi_set_timing) */
+    bool timing = false;
+    std::vector<hipEvent_t> ev_pool;
+    std::vector<std::pair<hipEvent_t, hipEvent_t>> ev_bake, ev_fold;
     int ngeneral = 0;
     float margin = 0;
     /* accumulation: FMGI_ACCUM_FX3 or FMGI_ACCUM_STATE (counts[1024][numTexels] + colour table) */
@@ -483,6 +491,9 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_gcells);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
+    for (hipEvent_t ev : c->ev_pool) hipEventDestroy(ev);
+    for (auto &p : c->ev_bake) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
+    for (auto &p : c->ev_fold) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     hipFree(c->d_src_item_begin);
     hipFree(c->d_src_launch0);
     hipFree(c->d_counts);
@@ -613,6 +624,11 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->grid_cells = (int)(gb.cells.size() / 2);
     c->grid_entries = (int)gb.idx.size();
     c->h_grid = gb;
+    {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
+           the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
+        const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
+        c->auto_kernel = (4 * slots < pairs) ? FMGI_KERNEL_GRID : FMGI_KERNEL_FAST;
+    }
     if (c->device != FMGI_HOST_ONLY) {
     HIPCHK(hipSetDevice(c->device));
     hipFree(c->d_rects);
@@ -764,6 +780,46 @@ static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace,
     return (int)std::max<uint64_t>(1, (lanes + block - 1) / block);
 }
 
+static hipError_t pool_event(fmgi_context *c, hipEvent_t &ev) {
+    if (!c->ev_pool.empty()) {
+        ev = c->ev_pool.back();
+        c->ev_pool.pop_back();
+        return hipSuccess;
+    }
+    return hipEventCreate(&ev);
+}
+
+/* with fmgi_set_timing on: an event before a launch ... */
+static hipError_t time_begin(fmgi_context *c, hipStream_t s, hipEvent_t &t0) {
+    if (!c->timing) return hipSuccess;
+    hipError_t e = pool_event(c, t0);
+    return e != hipSuccess ? e : hipEventRecord(t0, s);
+}
+
+/* ... and one after it, kept for fmgi_get_timing */
+static hipError_t time_end(fmgi_context *c, hipStream_t s, hipEvent_t t0, hipEvent_t &t1,
+                           std::vector<std::pair<hipEvent_t, hipEvent_t>> &dst) {
+    if (!c->timing) return hipSuccess;
+    hipError_t e = pool_event(c, t1);
+    if (e == hipSuccess) e = hipEventRecord(t1, s);
+    if (e == hipSuccess) dst.emplace_back(t0, t1);
+    return e;
+}
+
+/* work items per STREAM chunk: codes for 800 deposits per item, twice (stream + sorted), in at most half
+   of the device memory that is free or already held by the stream buffers */
+static uint64_t stream_chunk_items(fmgi_context *c) {
+    size_t fr = 0, tot = 0;
+    if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
+    const double avail = (double)fr + 8.0 * (double)c->sb_cap_alloc;
+    uint64_t items = (uint64_t)(avail * 0.5 / (2.0 * 4.0 * FMGI_EVENTS_PER_ITEM));
+    /* keep the fold's (tile, slice) table within 2^30 entries */
+    const uint64_t P = (uint64_t)((c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS);
+    const uint64_t max_items = ((1ull << 30) / std::max<uint64_t>(P, 1)) * FMGI_STREAM_SLICE / FMGI_EVENTS_PER_ITEM;
+    items = std::min(items, max_items);
+    return std::max<uint64_t>(items, 65536);
+}
+
 static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
                        void *events, int32_t *counts, uint32_t *rngf) {
     if (!c || !lm) return set_err(FMGI_ERR_ARG, "fmgi_bake_items: bad arguments");
@@ -771,7 +827,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (e > c->total_items || b > e) return set_err(FMGI_ERR_ARG, "item range [%llu,%llu) outside plan of %llu items",
                                                   (unsigned long long)b, (unsigned long long)e,
                                                   (unsigned long long)c->total_items);
-    if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_GRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
+    if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_AUTO) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
+    if (kernel == FMGI_KERNEL_AUTO) kernel = c->auto_kernel;
     if (b == e) return FMGI_OK;
     if (c->nrects == 0 || c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     HIPCHK(hipSetDevice(c->device));
@@ -815,18 +872,21 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int block = 256;
     if (c->accum != FMGI_ACCUM_STREAM) {
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
+        hipEvent_t t0 = nullptr, t1 = nullptr;
+        HIPCHK(time_begin(c, s, t0));
         HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid_blocks(c, kernel, c->accum, trace, block, e - b),
                                 block, s));
+        HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
         if (a.counts)
             HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
         return FMGI_OK;
     }
-    /* STREAM: at most kStreamChunkItems work items (4e8 photons; <= 12.8 GB of codes at the worst case
-       of 8 deposits per photon) per stream */
-    const uint64_t kStreamChunkItems = 4000000;
-    for (uint64_t cb = b; cb < e; cb += kStreamChunkItems) {
-        const uint64_t ce = std::min(e, cb + kStreamChunkItems);
+    /* STREAM: the codes of a chunk of work items are held in HBM (2 x 4 B per deposit, worst case 800
+       deposits per item); the chunk is sized from the free device memory (at most half of it) */
+    const uint64_t chunk = stream_chunk_items(c);
+    for (uint64_t cb = b; cb < e; cb += chunk) {
+        const uint64_t ce = std::min(e, cb + chunk);
         const int grid = grid_blocks(c, kernel, c->accum, trace, block, ce - cb);
         int rc = ensure_stream(c, ce - cb, grid, block);
         if (rc != FMGI_OK) return rc;
@@ -837,9 +897,47 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.stream_cursor = c->sb.cursor;
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         HIPCHK(hipMemsetAsync(c->sb.cursor, 0, 8, s));
+        hipEvent_t t0 = nullptr, t1 = nullptr;
+        HIPCHK(time_begin(c, s, t0));
         HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid, block, s));
+        HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
+        HIPCHK(time_begin(c, s, t0));
         HIPCHK(fmgi_stream_fold(c->sb, c->num_texels, c->d_colfx, (unsigned long long *)lm, s));
+        HIPCHK(time_end(c, s, t0, t1, c->ev_fold));
     }
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_auto_kernel(const fmgi_context *c) { return c ? c->auto_kernel : FMGI_ERR_ARG; }
+
+FMGI_API int fmgi_set_timing(fmgi_context *c, int on) {
+    if (!c) return set_err(FMGI_ERR_ARG, "null context");
+    c->timing = on != 0;
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_get_timing(fmgi_context *c, fmgi_timing *out) {
+    if (!c || !out) return set_err(FMGI_ERR_ARG, "fmgi_get_timing: bad arguments");
+    memset(out, 0, sizeof *out);
+    if (c->device == FMGI_HOST_ONLY) return FMGI_OK;
+    HIPCHK(hipSetDevice(c->device));
+    auto drain = [&](std::vector<std::pair<hipEvent_t, hipEvent_t>> &v, double &ms, uint64_t &n) -> hipError_t {
+        for (auto &p : v) {
+            hipError_t e = hipEventSynchronize(p.second);
+            if (e != hipSuccess) return e;
+            float t = 0;
+            e = hipEventElapsedTime(&t, p.first, p.second);
+            if (e != hipSuccess) return e;
+            ms += t;
+            n++;
+            c->ev_pool.push_back(p.first);
+            c->ev_pool.push_back(p.second);
+        }
+        v.clear();
+        return hipSuccess;
+    };
+    HIPCHK(drain(c->ev_bake, out->bake_ms, out->bake_launches));
+    HIPCHK(drain(c->ev_fold, out->fold_ms, out->fold_launches));
     return FMGI_OK;
 }
 
@@ -856,6 +954,17 @@ FMGI_API int fmgi_finalize(fmgi_context *c, const void *lm, const void *tin, voi
     HIPCHK(hipSetDevice(c->device));
     HIPCHK(fmgi_launch_finalize((const unsigned long long *)lm, (const float *)tin, (float *)tout, c->num_texels,
                                 stream ? (hipStream_t)stream : c->stream));
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_get_stage_cycles(fmgi_context *c, uint64_t out[16]) {
+    if (!c || !out) return set_err(FMGI_ERR_ARG, "fmgi_get_stage_cycles: bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    unsigned long long v[KSTAT_ALLOC];
+    HIPCHK(hipMemcpy(v, c->d_stats, sizeof v, hipMemcpyDeviceToHost));
+    for (int k = 0; k < 16; k++) out[k] = v[KSTAT_STAGE0 + k];
     return FMGI_OK;
 }
 
@@ -974,7 +1083,8 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     int wg = wg_env ? atoi(wg_env) : 256;
     if (wg <= 0) wg = 256;
     const char *k_env = getenv("FMGI_KERNEL");
-    int kernel = FMGI_KERNEL_GRID;
+    int kernel = FMGI_KERNEL_AUTO;
+    if (k_env && !strcmp(k_env, "grid")) kernel = FMGI_KERNEL_GRID;
     if (k_env && !strcmp(k_env, "exact")) kernel = FMGI_KERNEL_EXACT;
     if (k_env && !strcmp(k_env, "fast")) kernel = FMGI_KERNEL_FAST;
     int ndev = fmgi_device_count();

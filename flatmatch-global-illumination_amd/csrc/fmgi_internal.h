@@ -25,10 +25,11 @@ static_assert(sizeof(FilterRec) == 32, "FilterRec must be 32 B");
    their margin-grown extents. Cell (iu, iv) = cells[cell_off + iv*nu + iu] = {first record, count}. */
 struct GridPlane {
     float plane, u0, v0, iu; /* iu, iv = cells per unit length */
-    float iv;
+    float iv, mu, mv;        /* mu = nu - 1, mv = nv - 1 (the clamp bounds of the cell coordinates) */
     int32_t nu, nv, cell_off;
+    int32_t pad0, pad1;
 };
-static_assert(sizeof(GridPlane) == 32, "GridPlane must be 32 B");
+static_assert(sizeof(GridPlane) == 48, "GridPlane must be 48 B");
 
 struct BakeArgs {
     const RectDev *rects;
@@ -75,7 +76,7 @@ struct BakeArgs {
 };
 
 enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESCANS, KSTAT_TESTS, KSTAT_TIES,
-       KSTAT_INVALID, KSTAT_N, KSTAT_OVERFLOW = KSTAT_N, KSTAT_ALLOC = 16 };
+       KSTAT_INVALID, KSTAT_N, KSTAT_OVERFLOW = KSTAT_N, KSTAT_STAGE0 = 16, KSTAT_ALLOC = 32 };
 
 /* stream accumulation geometry (fmgi_accum.hip) */
 #define FMGI_STREAM_BLOCK 4096 /* codes reserved per wave at a time                         */

@@ -78,7 +78,26 @@ __device__ __forceinline__ float exact_at(const RectDev &r, f3 src, f3 dir, floa
 
 /* ---- scan policies -------------------------------------------------------------------------- */
 
+/* Stage timing (profiling builds only, -DFMGI_STAGE_TIMING): s_memtime deltas of each bake-loop stage,
+   summed per wave into stats[KSTAT_STAGE0 + k]; compiled out otherwise. */
+enum { ST_START = 0, ST_SAMPLE, ST_SCAN1, ST_SCAN2, ST_FALLBACK, ST_HIT, ST_APPEND, ST_N };
+struct StageClock {
+#ifdef FMGI_STAGE_TIMING
+    unsigned long long last = 0, acc[ST_N] = {};
+    __device__ __forceinline__ void lap(int k) {
+        const unsigned long long t = __builtin_amdgcn_s_memtime();
+        acc[k] += t - last;
+        last = t;
+    }
+    __device__ __forceinline__ void reset() { last = __builtin_amdgcn_s_memtime(); }
+#else
+    __device__ __forceinline__ void lap(int) {}
+    __device__ __forceinline__ void reset() {}
+#endif
+};
+
 struct ScanStats {
+    StageClock clk;
     unsigned long long tests = 0;    /* rectangle tests evaluated (phase-1 records + exact tests)   */
     unsigned long long rescans = 0;  /* fast scan: scans re-done by the literal exact scan          */
     unsigned long long ties = 0;     /*   ... because the runner-up was within the separation band */
@@ -209,6 +228,31 @@ struct ScanFast {
  * its separation argument carry over unchanged. A closed box of 200 rects has 6 planes: ~3 cells and a
  * few records per scan instead of ~100 rect tests.
  */
+/* The kernel's cell of hit point (uh, vh) on plane record g (48 B, see GridPlane). */
+__device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, const float4 g2, float uh, float vh) {
+    /* g0 = {plane, u0, v0, iu}, g1 = {iv, mu, mv, nu}, g2 = {nv, cell_off, -, -} */
+    const float tu = fminf(fmaxf((uh - g0.y) * g0.w, 0.0f), g1.y);
+    const float tv = fminf(fmaxf((vh - g0.z) * g1.x, 0.0f), g1.z);
+    return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)tv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)tu;
+}
+
+/* one candidate test of ScanGrid's phase 1: record r against hit point (uh, vh) at fac' f */
+__device__ __forceinline__ void grid_rec(float f, float uh, float vh, float4 r, int code, float &L1, float &L2,
+                                         int &code1) {
+    const bool ok = (int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w);
+    const float key = ok ? f : INFINITY;
+    const bool lt = key < L1;
+    L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+    code1 = lt ? code : code1;
+    L1 = lt ? key : L1;
+}
+
+/*
+ * Phase 1 of ScanGrid on the planes of axis A: per facing plane, fac' and the hit point once, the cell
+ * it falls in, and the records of that cell (the first two loaded together with no wait in between).
+ * The LDS image holds, per axis, pairs {+A plane j, -A plane j} of 48-B GridPlane records; a lane reads
+ * the one its direction faces.
+ */
 template <int A>
 __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, int J, f3 s, f3 d, float &L1,
                                           float &L2, int &code1, unsigned &ntest) {
@@ -217,29 +261,20 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
-    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 32), 16);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
     const uint2 *cells = (const uint2 *)a.gcells;
     const float4 *recs = (const float4 *)a.grecs;
     for (int j = 0; j < J; j++) {
-        const float4 q0 = p[4 * j];     /* plane, u0, v0, iu */
-        const float4 q1 = p[4 * j + 1]; /* iv, nu, nv, cell_off */
-        const float f = (q0.x - sa) * rd;
+        const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
+        const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue; /* plane behind the photon (or NaN): no candidate on it */
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        const int nu = __float_as_int(q1.y), nv = __float_as_int(q1.z), off = __float_as_int(q1.w);
-        const float tu = fminf(fmaxf((uh - q0.y) * q0.w, 0.0f), (float)(nu - 1));
-        const float tv = fminf(fmaxf((vh - q0.z) * q1.x, 0.0f), (float)(nv - 1));
-        const uint2 c = cells[off + (int)tv * nu + (int)tu];
+        const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
+        const float4 r0 = recs[c.y > 0 ? c.x : 0], r1 = recs[c.y > 1 ? c.x + 1 : 0];
         ntest += c.y;
-        for (uint32_t k = 0; k < c.y; k++) {
-            const float4 r = recs[c.x + k];
-            const bool ok = (int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w);
-            const float key = ok ? f : INFINITY;
-            const bool lt = key < L1;
-            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
-            code1 = lt ? (int)(c.x + k) : code1;
-            L1 = lt ? key : L1;
-        }
+        if (c.y > 0) grid_rec(f, uh, vh, r0, (int)c.x, L1, L2, code1);
+        if (c.y > 1) grid_rec(f, uh, vh, r1, (int)c.x + 1, L1, L2, code1);
+        for (uint32_t k = 2; k < c.y; k++) grid_rec(f, uh, vh, recs[c.x + k], (int)(c.x + k), L1, L2, code1);
     }
 }
 
@@ -251,19 +286,15 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, i
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
-    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 32), 16);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
     const uint2 *cells = (const uint2 *)a.gcells;
     const float4 *recs = (const float4 *)a.grecs;
     for (int j = 0; j < J; j++) {
-        const float4 q0 = p[4 * j];
-        const float4 q1 = p[4 * j + 1];
-        const float f = (q0.x - sa) * rd;
+        const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
+        const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        const int nu = __float_as_int(q1.y), nv = __float_as_int(q1.z), off = __float_as_int(q1.w);
-        const float tu = fminf(fmaxf((uh - q0.y) * q0.w, 0.0f), (float)(nu - 1));
-        const float tv = fminf(fmaxf((vh - q0.z) * q1.x, 0.0f), (float)(nv - 1));
-        const uint2 c = cells[off + (int)tv * nu + (int)tu];
+        const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
         for (uint32_t k = 0; k < c.y; k++) {
             const float4 r = recs[c.x + k];
             if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[c.x + k]);
@@ -289,8 +320,8 @@ struct ScanGrid {
             int nxt = INT_MAX;
             auto take = [&](int idx) { nxt = (idx > prev && idx < nxt) ? idx : nxt; };
             grid_visit<0>(a, lds, a.fJ[0], src, dir, take);
-            grid_visit<1>(a, lds + 64 * a.fJ[0], a.fJ[1], src, dir, take);
-            grid_visit<2>(a, lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
+            grid_visit<1>(a, lds + 96 * a.fJ[0], a.fJ[1], src, dir, take);
+            grid_visit<2>(a, lds + 96 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
             for (int g = 0; g < a.ngeneral; g++) {
                 const int idx = a.general[g];
                 if (idx > prev && idx < nxt && exact_on(R, idx, src, dir, INFINITY) >= 0) nxt = idx;
@@ -315,8 +346,8 @@ struct ScanGrid {
         int code1 = -1;
         unsigned ntest = 0;
         grid_axis<0>(a, lds, a.fJ[0], src, dir, L1, L2, code1, ntest);
-        grid_axis<1>(a, lds + 64 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
-        grid_axis<2>(a, lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
+        grid_axis<1>(a, lds + 96 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
+        grid_axis<2>(a, lds + 96 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;
         for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
@@ -328,21 +359,25 @@ struct ScanGrid {
             L1 = lt ? key : L1;
         }
         st.tests += (unsigned long long)(ntest + (unsigned)a.ngeneral);
+        st.clk.lap(ST_SCAN1);
         if (L1 == INFINITY) {
             best = INFINITY;
             return -1;
         }
         const int idx = code1 >= 0 ? a.gridx[code1] : a.general[-2 - code1];
         const float f = exact_at(a.rects[idx], src, dir, INFINITY);
-        if (!(f < 0) && L2 > f * 1.000244140625f) { /* ScanFast's separation test */
+        const bool sep = !(f < 0) && L2 > f * 1.000244140625f; /* ScanFast's separation test */
+        st.clk.lap(ST_SCAN2);
+        if (sep) {
             best = f;
             return idx;
         }
         st.rescans++;
         if (f < 0) st.invalid++; else st.ties++;
-        const int r = ordered_exact(a, lds, src, dir, best);
-        if (r != -2) return r;
-        return ScanExact::scan(a, lds, src, dir, best, st);
+        int r = ordered_exact(a, lds, src, dir, best);
+        if (r == -2) r = ScanExact::scan(a, lds, src, dir, best, st);
+        st.clk.lap(ST_FALLBACK);
+        return r;
     }
 };
 
@@ -463,8 +498,13 @@ __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
  * its two draws are skipped with one LCG jump. Per lane, RNG draws happen in exactly the reference
  * order: roulette (:236), bounce sample (:238), then the next photon's dx, dy (:173-174) and sample.
  */
+#ifdef FMGI_WAVES_PER_EU /* experiment builds: ask the register allocator for this occupancy */
+#define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(FMGI_WAVES_PER_EU)))
+#else
+#define FMGI_BAKE_ATTR
+#endif
 template <class Scan, class Acc, bool TRACE>
-__global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
+__global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
     if (Scan::kLds) { /* stage the filter image once per workgroup */
         const int n16 = a.fimg_bytes >> 4;
@@ -482,6 +522,7 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
     ScanStats sst;
     WaveStream ws;
 
+    sst.clk.reset();
     for (;;) {
         /* ---- stage 1: new photon (and new work item), then the iteration's one direction sample ---- */
         float edx = 0, edy = 0;
@@ -520,6 +561,7 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
             depth = 0;
             n_ph++;
         }
+        sst.clk.lap(ST_START);
         if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
         if (start) {
             const SrcDev &S = a.srcs[srci];
@@ -531,11 +573,13 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         }
         start = false;
         pend = false;
+        sst.clk.lap(ST_SAMPLE);
 
         /* ---- stage 2: scan ---- */
         float best;
         const int hit = Scan::scan(a, s_img, pos, dir, best, sst);
         n_scan++;
+        sst.clk.lap(ST_SCAN1); /* scans without an inner split (ScanExact / ScanFast) */
         bool dep = false;
         uint32_t code = 0;
         if (best == INFINITY) { /* photonmap.cl:208-209 */
@@ -589,7 +633,9 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         if (last) start = true;
         depth++;
         }
+        sst.clk.lap(ST_HIT);
         if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, dep, code);
+        sst.clk.lap(ST_APPEND);
     }
     if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws);
     if (TRACE && photon >= 0) {
@@ -603,6 +649,10 @@ __global__ __launch_bounds__(1024) void k_bake(BakeArgs a) {
         unsigned long long s = wave_sum(v[i]);
         if ((threadIdx.x & 63) == 0 && s) atomicAdd(a.stats + i, s);
     }
+#ifdef FMGI_STAGE_TIMING
+    if ((threadIdx.x & 63) == 0)
+        for (int k = 0; k < ST_N; k++) atomicAdd(a.stats + KSTAT_STAGE0 + k, sst.clk.acc[k]);
+#endif
 }
 
 /* AccState -> int64 fixed point: lm[t][c] += sum_s counts[s][t] * colour_fx[s][c]; counts zeroed.

@@ -18,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import scene
-from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, FmgiError, Geometry, Stats,
+from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, Timing, FmgiError, Geometry, Stats,
                    check, load)
 from .scene import RECT_DTYPE, Scene
 
@@ -43,6 +43,7 @@ __all__ = [
     "KERNEL_EXACT",
     "KERNEL_FAST",
     "KERNEL_GRID",
+    "KERNEL_AUTO",
     "ACCUM_AUTO",
     "ACCUM_FX3",
     "ACCUM_STATE",
@@ -142,7 +143,7 @@ class Context:
         check(self.lib.fmgi_get_plan(self.h, _ptr(out), len(out)), "fmgi_get_plan")
         return out
 
-    def bake_items(self, begin: int, end: int, lm_fx_ptr: int, kernel: int = KERNEL_GRID, stream: int = 0):
+    def bake_items(self, begin: int, end: int, lm_fx_ptr: int, kernel: int = KERNEL_AUTO, stream: int = 0):
         """Launch on `stream` (a hipStream_t as int; pass the stream that produced lm_fx). 0/None selects
         the context's internal stream, which is NOT ordered with torch's default stream."""
         check(self.lib.fmgi_bake_items(self.h, begin, end, C.c_void_p(lm_fx_ptr), kernel, C.c_void_p(stream or None)),
@@ -163,7 +164,7 @@ class Context:
     def reset_stats(self):
         check(self.lib.fmgi_reset_stats(self.h), "fmgi_reset_stats")
 
-    def trace_items(self, begin: int, end: int, kernel: int = KERNEL_GRID):
+    def trace_items(self, begin: int, end: int, kernel: int = KERNEL_AUTO):
         """Per-photon bounce records of items [begin, end): (events[n, 800], counts[n], rng_final[n])."""
         n = end - begin
         ev = np.zeros(n * EVENTS_PER_ITEM, EVENT_DTYPE)
@@ -171,6 +172,19 @@ class Context:
         rng = np.zeros(n, np.uint32)
         check(self.lib.fmgi_trace_items(self.h, begin, end, kernel, _ptr(ev), _ptr(cnt), _ptr(rng)), "fmgi_trace_items")
         return ev.reshape(n, EVENTS_PER_ITEM), cnt, rng
+
+    @property
+    def auto_kernel(self) -> int:
+        return int(self.lib.fmgi_auto_kernel(self.h))
+
+    def set_timing(self, on: bool = True):
+        check(self.lib.fmgi_set_timing(self.h, 1 if on else 0), "fmgi_set_timing")
+
+    def timing(self) -> dict:
+        """Device time of the bake / fold launches since the previous call (needs set_timing(True))."""
+        t = Timing()
+        check(self.lib.fmgi_get_timing(self.h, C.byref(t)), "fmgi_get_timing")
+        return t.as_dict()
 
     def grid_tables(self) -> dict:
         """FMGI_KERNEL_GRID's plane/cell/record tables (include/flatmatch_gi.h fmgi_grid_copy)."""
@@ -194,8 +208,9 @@ class Context:
 
 
 GRID_PLANE_DTYPE = np.dtype([("plane", "<f4"), ("u0", "<f4"), ("v0", "<f4"), ("iu", "<f4"), ("iv", "<f4"),
-                             ("nu", "<i4"), ("nv", "<i4"), ("cell_off", "<i4")])
-assert GRID_PLANE_DTYPE.itemsize == 32
+                             ("mu", "<f4"), ("mv", "<f4"), ("nu", "<i4"), ("nv", "<i4"), ("cell_off", "<i4"),
+                             ("pad0", "<i4"), ("pad1", "<i4")])
+assert GRID_PLANE_DTYPE.itemsize == 48
 
 
 def make_geometry(sc: Scene, texels: np.ndarray):

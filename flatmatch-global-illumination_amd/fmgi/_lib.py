@@ -6,7 +6,10 @@ import ctypes as C
 import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-LIB_PATH = os.path.join(PKG_DIR, "libflatmatch_gi.so")
+# FMGI_LIB=<name> selects a profiling/experiment build libflatmatch_gi_<name>.so (make -C <pkg> timing,
+# make -C <pkg> variant VNAME=<name> VFLAGS=...); the product and every test use libflatmatch_gi.so
+LIB_PATH = os.path.join(PKG_DIR, f"libflatmatch_gi_{os.environ['FMGI_LIB']}.so" if os.environ.get("FMGI_LIB")
+                        else "libflatmatch_gi.so")
 
 # Exported symbols of the C ABI (tests check the built library exports exactly these + nothing
 # that would clash with the reference objects main.c links against).
@@ -33,11 +36,16 @@ EXPORTS = (
     "fmgi_device_sincosf",
     "fmgi_grid_sizes",
     "fmgi_grid_copy",
+    "fmgi_get_stage_cycles",
+    "fmgi_auto_kernel",
+    "fmgi_set_timing",
+    "fmgi_get_timing",
 )
 
 KERNEL_EXACT = 0
 KERNEL_FAST = 1
 KERNEL_GRID = 2
+KERNEL_AUTO = 3
 ACCUM_AUTO = 0
 ACCUM_FX3 = 1
 ACCUM_STATE = 2
@@ -64,6 +72,18 @@ class Stats(C.Structure):
 
     def as_dict(self):
         return {k: int(getattr(self, k)) for k, _ in self._fields_}
+
+
+class Timing(C.Structure):
+    _fields_ = [
+        ("bake_ms", C.c_double),
+        ("fold_ms", C.c_double),
+        ("bake_launches", C.c_uint64),
+        ("fold_launches", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: (float if k.endswith("ms") else int)(getattr(self, k)) for k, _ in self._fields_}
 
 
 class Geometry(C.Structure):
@@ -121,6 +141,10 @@ def load() -> C.CDLL:
         "fmgi_host_sincosf": (None, [vp, vp, vp, i64]),
         "fmgi_device_sincosf": (C.c_int, [vp, vp, vp, vp, i64]),
         "fmgi_grid_sizes": (C.c_int, [vp, vp]),
+        "fmgi_get_stage_cycles": (C.c_int, [vp, vp]),
+        "fmgi_auto_kernel": (C.c_int, [vp]),
+        "fmgi_set_timing": (C.c_int, [vp, C.c_int]),
+        "fmgi_get_timing": (C.c_int, [vp, C.POINTER(Timing)]),
         "fmgi_grid_copy": (C.c_int, [vp, vp, vp, vp, vp]),
         "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
         "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),

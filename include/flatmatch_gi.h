@@ -21,7 +21,7 @@
  *   FMGI_WG        virtual OpenCL work-group size of the launch schedule (default 256, the value
  *                  ROCm's OpenCL reports for CL_KERNEL_WORK_GROUP_SIZE; global_illumination_cl.c:300)
  *   FMGI_GPUS      number of GPUs to shard over (default: all visible, max 8)
- *   FMGI_KERNEL    "grid" (default), "fast" or "exact" -- all produce identical bits; see DESIGN.md
+ *   FMGI_KERNEL    "auto" (default), "grid", "fast" or "exact" -- all produce identical bits; see DESIGN.md
  *   FMGI_QUIET     1 = suppress the reference's progress line
  */
 #ifndef FLATMATCH_GI_H
@@ -74,7 +74,8 @@ enum {
 
 /* Scan kernels (identical bits): EXACT = photonmap.cl's scan over every rect; FAST = conservative fp32
    filter over every rect + exact verification; GRID = FAST's filter over per-plane grid cells only. */
-enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2 };
+enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2, FMGI_KERNEL_AUTO = 3 };
+/* AUTO = GRID when the scene has few planes for its rect count (closed boxes), else FAST. */
 /* Deposit accumulation (both exact and order-free; results are identical):
    FX3   three int64 fixed-point atomics per deposit into the lightmap;
    STATE one u64 atomic per deposit into counts[colour state][texel] (8 KiB per texel of device memory),
@@ -160,6 +161,18 @@ int fmgi_bake_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, v
    .s[3] copied. Either texel pointer may alias. */
 int fmgi_finalize(fmgi_context *ctx, const void *lm_fx_dev, const void *texels_in_dev, void *texels_out_dev,
                   void *stream);
+/* The kernel FMGI_KERNEL_AUTO resolves to for the current scene. */
+int fmgi_auto_kernel(const fmgi_context *ctx);
+/* Device-side timing of the bake's kernels (HIP events around each launch, on the bake's stream), off
+   by default. fmgi_get_timing synchronises, returns the sums since the previous call and resets them. */
+typedef struct {
+    double bake_ms;         /* k_bake launches                                   */
+    double fold_ms;         /* STREAM fold (hist + scan + scatter + accumulate)  */
+    uint64_t bake_launches;
+    uint64_t fold_launches;
+} fmgi_timing;
+int fmgi_set_timing(fmgi_context *ctx, int on);
+int fmgi_get_timing(fmgi_context *ctx, fmgi_timing *out);
 /* Counters of all bakes since the last reset (synchronises the context's device). */
 int fmgi_get_stats(fmgi_context *ctx, fmgi_stats *out);
 int fmgi_reset_stats(fmgi_context *ctx);
@@ -173,10 +186,15 @@ int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, 
    tooling. sizes[0..2] = plane pairs per axis (x, y, z), sizes[3] = cells, sizes[4] = cell entries.
    fmgi_grid_copy fills (any pointer may be NULL):
      planes[2 * (sizes[0] + sizes[1] + sizes[2])]: per axis, pairs {plane of the +n class, plane of the
-       -n class}, each {float plane, u0, v0, iu, iv; int32 nu, nv, cell_off} (32 B; NaN plane = padding);
+       -n class}, each {float plane, u0, v0, iu, iv, mu, mv; int32 nu, nv, cell_off, pad[2]} (48 B;
+       mu = nu - 1, mv = nv - 1; NaN plane = padding);
      cells[2 * sizes[3]]: {first entry, count}; recs[4 * sizes[4]]: {cu, hwu, cv, hwv} (margin-grown
      extents); idx[sizes[4]]: rect index. */
 int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);
+/* Profiling builds only (make timing -> libflatmatch_gi_timing.so, -DFMGI_STAGE_TIMING): shader-clock
+   cycles summed over waves per bake-loop stage {start, sample, scan phase 1, phase 2, fallback, hit,
+   append}, since the last fmgi_reset_stats; all zero in the normal library. */
+int fmgi_get_stage_cycles(fmgi_context *ctx, uint64_t out[16]);
 int fmgi_grid_copy(const fmgi_context *ctx, void *planes, uint32_t *cells, float *recs, int32_t *idx);
 
 /* Host helpers exported for tests (no device needed). */

@@ -34,8 +34,9 @@ def _planes(t):
 def _cell_of(p, u, v):
     """The kernel's cell index for hit point (u, v): fminf(fmaxf((x - o) * inv, 0), n - 1), truncated."""
     f32 = np.float32
-    tu = np.minimum(np.maximum((u - f32(p["u0"])) * f32(p["iu"]), f32(0)), f32(p["nu"] - 1))
-    tv = np.minimum(np.maximum((v - f32(p["v0"])) * f32(p["iv"]), f32(0)), f32(p["nv"] - 1))
+    assert p["mu"] == p["nu"] - 1 and p["mv"] == p["nv"] - 1
+    tu = np.minimum(np.maximum((u - f32(p["u0"])) * f32(p["iu"]), f32(0)), f32(p["mu"]))
+    tv = np.minimum(np.maximum((v - f32(p["v0"])) * f32(p["iv"]), f32(0)), f32(p["mv"]))
     return tv.astype(np.int64) * int(p["nu"]) + tu.astype(np.int64)
 
 
