@@ -420,10 +420,11 @@ struct fmgi_context {
     int accum = FMGI_ACCUM_FX3;
     unsigned long long *d_counts = nullptr;
     long long *d_colfx = nullptr;
+    uint32_t *d_colpack = nullptr; /* the same table as u32 {r, g, b, 0} (STREAM fold) */
     /* STREAM: deposit-code stream + fold buffers, grown on demand (fmgi_accum.hip) */
     StreamBufs sb{};
     uint64_t sb_cap_alloc = 0;
-    int sb_entries_alloc = 0;
+    uint64_t sb_entries_alloc = 0;
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -501,9 +502,8 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->sb.stream);
     hipFree(c->sb.sorted);
     hipFree(c->sb.cursor);
-    hipFree(c->sb.hist);
-    hipFree(c->sb.offs);
-    hipFree(c->sb.scan_tmp);
+    hipFree(c->sb.toff);
+    hipFree(c->d_colpack);
     hipFree(c->d_counter);
     hipFree(c->d_stats);
     if (c->stream) hipStreamDestroy(c->stream);
@@ -518,8 +518,17 @@ static const int kStreamMaxTexels = FMGI_MAX_TILES << FMGI_TILE_BITS; /* 4,194,3
 static int ensure_colour_table(fmgi_context *c) {
     if (c->d_colfx) return FMGI_OK;
     std::vector<long long> t = colour_table();
+    std::vector<uint32_t> p((size_t)FMGI_COLOUR_STATES * 4, 0u);
+    for (int sid = 0; sid < FMGI_COLOUR_STATES; sid++)
+        for (int k = 0; k < 3; k++) {
+            const long long v = t[3 * sid + k]; /* <= 18 * 2^25 < 2^32 */
+            if (v < 0 || v > (long long)UINT32_MAX) return set_err(FMGI_ERR_STATE, "colour table overflow");
+            p[4 * sid + k] = (uint32_t)v;
+        }
     HIPCHK(hipMalloc(&c->d_colfx, t.size() * sizeof(long long)));
     HIPCHK(hipMemcpy(c->d_colfx, t.data(), t.size() * sizeof(long long), hipMemcpyHostToDevice));
+    HIPCHK(hipMalloc(&c->d_colpack, p.size() * sizeof(uint32_t)));
+    HIPCHK(hipMemcpy(c->d_colpack, p.data(), p.size() * sizeof(uint32_t), hipMemcpyHostToDevice));
     return FMGI_OK;
 }
 
@@ -555,9 +564,7 @@ static int ensure_stream(fmgi_context *c, uint64_t items, int grid, int block) {
     const uint64_t cap = items * FMGI_EVENTS_PER_ITEM + (waves + 1) * FMGI_STREAM_BLOCK;
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
     const uint64_t nslices = (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
-    const uint64_t entries = (uint64_t)P * nslices + 1;
-    if (entries > (uint64_t)INT32_MAX) return set_err(FMGI_ERR_ARG, "stream fold too large (%llu entries)",
-                                                     (unsigned long long)entries);
+    const uint64_t entries = (uint64_t)(P + 1) * nslices;
     if (cap > c->sb_cap_alloc) {
         hipFree(c->sb.stream);
         hipFree(c->sb.sorted);
@@ -567,22 +574,17 @@ static int ensure_stream(fmgi_context *c, uint64_t items, int grid, int block) {
         HIPCHK(hipMalloc(&c->sb.sorted, cap * sizeof(uint32_t)));
         c->sb_cap_alloc = cap;
     }
-    if ((int)entries > c->sb_entries_alloc) {
-        hipFree(c->sb.hist);
-        hipFree(c->sb.offs);
-        hipFree(c->sb.scan_tmp);
-        c->sb.hist = c->sb.offs = nullptr;
-        c->sb.scan_tmp = nullptr;
+    if (entries > c->sb_entries_alloc) {
+        hipFree(c->sb.toff);
+        c->sb.toff = nullptr;
         c->sb_entries_alloc = 0;
-        HIPCHK(hipMalloc(&c->sb.hist, entries * sizeof(unsigned long long)));
-        HIPCHK(hipMalloc(&c->sb.offs, entries * sizeof(unsigned long long)));
-        c->sb.scan_tmp_bytes = fmgi_stream_scan_bytes((int)entries);
-        HIPCHK(hipMalloc(&c->sb.scan_tmp, std::max<size_t>(c->sb.scan_tmp_bytes, 16)));
-        c->sb_entries_alloc = (int)entries;
+        HIPCHK(hipMalloc(&c->sb.toff, entries * sizeof(uint16_t)));
+        c->sb_entries_alloc = entries;
     }
     if (!c->sb.cursor) HIPCHK(hipMalloc(&c->sb.cursor, 64));
     c->sb.cap = cap;
-    c->sb.accum_blocks = c->num_cus * 2;
+    c->sb.colpack = c->d_colpack;
+    c->sb.groups = std::max(1, (2 * c->num_cus + P - 1) / P); /* ~2 sum workgroups per CU */
     return FMGI_OK;
 }
 
@@ -813,9 +815,8 @@ static uint64_t stream_chunk_items(fmgi_context *c) {
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
     const double avail = (double)fr + 8.0 * (double)c->sb_cap_alloc;
     uint64_t items = (uint64_t)(avail * 0.5 / (2.0 * 4.0 * FMGI_EVENTS_PER_ITEM));
-    /* keep the fold's (tile, slice) table within 2^30 entries */
-    const uint64_t P = (uint64_t)((c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS);
-    const uint64_t max_items = ((1ull << 30) / std::max<uint64_t>(P, 1)) * FMGI_STREAM_SLICE / FMGI_EVENTS_PER_ITEM;
+    /* slices are indexed in 32 bits by the sort kernel's grid */
+    const uint64_t max_items = ((1ull << 31) - 1) / FMGI_EVENTS_PER_ITEM * FMGI_STREAM_SLICE;
     items = std::min(items, max_items);
     return std::max<uint64_t>(items, 65536);
 }
@@ -902,7 +903,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid, block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_stream_fold(c->sb, c->num_texels, c->d_colfx, (unsigned long long *)lm, s));
+        HIPCHK(fmgi_stream_fold(c->sb, c->num_texels, (unsigned long long *)lm, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_fold));
     }
     return FMGI_OK;

@@ -85,19 +85,15 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 #define FMGI_MAX_TILES 1024    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */
 
 struct StreamBufs {
-    uint32_t *stream;               /* deposit codes, cap entries                     */
+    uint32_t *stream;           /* deposit codes, cap entries                                   */
     uint64_t cap;
-    unsigned long long *cursor;     /* reserved codes (device)                        */
-    uint32_t *sorted;               /* codes sorted by tile, cap entries              */
-    unsigned long long *hist;       /* [tiles * slices + 1] counts, then ...          */
-    unsigned long long *offs;       /* ... their exclusive scan                       */
-    void *scan_tmp;
-    size_t scan_tmp_bytes;
-    int accum_blocks;
+    unsigned long long *cursor; /* reserved codes (device)                                      */
+    uint32_t *sorted;           /* per 8192-code slice: its codes sorted by tile, cap entries    */
+    uint16_t *toff;             /* per slice: P + 1 run offsets (the last = valid codes)        */
+    const uint32_t *colpack;    /* colour table as u32 {r, g, b, 0} per state (fixed point)      */
+    int groups;                 /* slice groups per tile in the sum kernel                      */
 };
-hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, const long long *colfx, unsigned long long *lm,
-                            hipStream_t s);
-size_t fmgi_stream_scan_bytes(int entries);
+hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);
 
 #define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
 
