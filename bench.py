@@ -79,10 +79,10 @@ def pmc_traffic(config_name):
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p))
-        return d.get(config_name, {}).get("hbm_bytes_per_launch")
-    except Exception:
+        d = json.load(open(p)).get(config_name, {})
+    except (OSError, ValueError):
         return None
+    return d.get("hbm_bytes_per_launch") if "k_bake" in d.get("kernel", "") else None
 
 
 def main():
