@@ -55,6 +55,13 @@ int set_err(int code, const char *fmt, ...) {
         if (e_ != hipSuccess) return set_err(FMGI_ERR_HIP, "%s: %s", #expr, hipGetErrorString(e_));    \
     } while (0)
 
+} // namespace
+
+/* fmgi_last_error() for the other host translation units (fmgi_ao_host.cpp) */
+int internal_set_err(int code, const char *msg) { return set_err(code, "%s", msg); }
+
+namespace {
+
 f3 v3of(const fmgi_vec3 &v) { return mkf3(v.s[0], v.s[1], v.s[2]); }
 
 /* Host restatement of the per-rectangle values photonmap.cl recomputes per test (bit-identical). */

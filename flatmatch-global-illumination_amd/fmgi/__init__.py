@@ -234,3 +234,43 @@ def bake_geometry(sc: Scene, spa: int, texels: np.ndarray | None = None) -> np.n
     check(load().getGlobalIlluminationCl(C.byref(g), spa, out.ctypes.data_as(C.c_void_p)), "getGlobalIlluminationCl")
     del keep
     return out
+
+
+# ---- ambient occlusion (include/flatmatch_gi.h) ----------------------------------
+
+def ambient_occlusion(sc: Scene, wall_begin: int = 0, wall_end: int | None = None,
+                      texels: np.ndarray | None = None) -> np.ndarray:
+    """The reference's performAmbientOcclusionNative on the GPU (fmgi_ambient_occlusion): returns
+    float32 [numTexels, 4] = `texels` (default zeros) with the level-0 texels of walls
+    [wall_begin, wall_end) replaced by (d, d, d, 0)."""
+    lib = load()
+    tex = np.zeros((sc.num_texels, 4), np.float32) if texels is None else np.ascontiguousarray(texels, np.float32)
+    out = np.empty_like(tex)
+    g, keep = make_geometry(sc, tex)
+    we = len(sc.walls) if wall_end is None else wall_end
+    check(lib.fmgi_ambient_occlusion(C.byref(g), wall_begin, we, _ptr(out)), "fmgi_ambient_occlusion")
+    return out
+
+
+def geosphere(levels: int = 4) -> np.ndarray:
+    """The AO direction table (fmgi_geosphere): float32 [n, 3] in the reference's order."""
+    lib = load()
+    n = lib.fmgi_geosphere(levels, None, 0)
+    if n < 0:
+        raise FmgiError(lib.fmgi_last_error().decode())
+    out = np.zeros((n, 3), np.float32)
+    lib.fmgi_geosphere(levels, _ptr(out), n)
+    return out
+
+
+def ao_tree(sc: Scene) -> np.ndarray:
+    """The AO BSP tree (fmgi_ao_tree encoding)."""
+    lib = load()
+    tex = np.zeros((sc.num_texels, 4), np.float32)
+    g, keep = make_geometry(sc, tex)
+    n = lib.fmgi_ao_tree(C.byref(g), None, 0)
+    if n < 0:
+        raise FmgiError(lib.fmgi_last_error().decode())
+    out = np.zeros(max(n, 1), np.int32)
+    lib.fmgi_ao_tree(C.byref(g), _ptr(out), n)
+    return out[:n]

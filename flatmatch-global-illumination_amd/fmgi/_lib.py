@@ -40,6 +40,10 @@ EXPORTS = (
     "fmgi_auto_kernel",
     "fmgi_set_timing",
     "fmgi_get_timing",
+    "performAmbientOcclusionGpu",
+    "fmgi_ambient_occlusion",
+    "fmgi_geosphere",
+    "fmgi_ao_tree",
 )
 
 KERNEL_EXACT = 0
@@ -145,6 +149,10 @@ def load() -> C.CDLL:
         "fmgi_auto_kernel": (C.c_int, [vp]),
         "fmgi_set_timing": (C.c_int, [vp, C.c_int]),
         "fmgi_get_timing": (C.c_int, [vp, C.POINTER(Timing)]),
+        "performAmbientOcclusionGpu": (None, [vp]),
+        "fmgi_ambient_occlusion": (C.c_int, [vp, C.c_int, C.c_int, vp]),
+        "fmgi_geosphere": (C.c_int, [C.c_int, vp, C.c_int]),
+        "fmgi_ao_tree": (i64, [vp, vp, i64]),
         "fmgi_grid_copy": (C.c_int, [vp, vp, vp, vp, vp]),
         "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
         "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),

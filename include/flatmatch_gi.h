@@ -62,6 +62,24 @@ void performGlobalIlluminationCl(fmgi_geometry *geo, int numSamplesPerArea);
    Returns 0 on success, a negative fmgi error code otherwise (no exit()). */
 int getGlobalIlluminationCl(const fmgi_geometry *geo, int numSamplesPerArea, fmgi_vec3 *texels_out);
 
+/* ---- Ambient occlusion ------------------------------------------------------ */
+/* The reference's performAmbientOcclusionNative (global_illumination_native.h:16, photonmap.c:478-490)
+   on the GPU, bit-identical: every level-0 texel of every wall becomes (d, d, d, 0), d the
+   cosine-weighted mean distance over the 481 geoSphere4 directions (misses count 10), traced through
+   the reference's BSP tree. Same argument meaning and in-place update; a different name, because the
+   reference's photonmap.o (which main.c also needs for performPhotonMappingNative) already defines
+   performAmbientOcclusionNative. Fatal errors print "[Err] ..." and exit(-1). */
+void performAmbientOcclusionGpu(fmgi_geometry *geo);
+/* Non-mutating form for walls [wall_begin, wall_end) (the BSP always spans every wall):
+   texels_out = geo->texels with those walls' level-0 texels replaced. Returns 0 or FMGI_ERR_*. */
+int fmgi_ambient_occlusion(const fmgi_geometry *geo, int wall_begin, int wall_end, fmgi_vec3 *texels_out);
+/* The direction table of `levels` subdivisions (4 = the AO table, 481 directions) in the reference's
+   order, as xyz float triples; returns the count and copies at most `cap` directions. */
+int fmgi_geosphere(int levels, float *xyz, int cap);
+/* The AO BSP tree, encoded per node as {left, right, plane wall, n, n wall indices}; returns the
+   encoding's length and copies at most `cap` ints. */
+int64_t fmgi_ao_tree(const fmgi_geometry *geo, int32_t *out, int64_t cap);
+
 /* ---- Build-defined device-resident API ---------------------------------------------------------- */
 enum {
     FMGI_OK = 0,

@@ -9,6 +9,8 @@
 #                                clBuildProgram (global_illumination_cl.c:196: -cl-fast-relaxed-math).
 #   _ref/dump_geometry           reference parseLayout.c/image.c/png_helper.c/rectangle.c/... +
 #                                oracle/dump_geometry.c; turns a layout PNG into a geometry fixture.
+#   _ref/ao_ref                  reference photonmap.c/rectangle.c/vector3_cl.c/geoSphere.c + oracle/ao_ref_main.c:
+#                                performAmbientOcclusionNative on a geometry fixture (AO fixtures).
 #   _ref/globalIllumination_fmgi reference main.c + its layout/IO objects linked against OUR
 #                                libflatmatch_gi.so instead of global_illumination_cl.o (drop-in check).
 #
@@ -46,6 +48,10 @@ done
 gcc $CFLAGS -c "$HERE/dump_geometry.c" -o "$OUT/obj/dump_geometry.o"
 COMMON="$OUT/obj/parseLayout.o $OUT/obj/image.o $OUT/obj/png_helper.o $OUT/obj/rectangle.o $OUT/obj/geometry.o $OUT/obj/vector3_cl.o $OUT/obj/helpers.o"
 gcc -o "$OUT/dump_geometry" "$OUT/obj/dump_geometry.o" $COMMON "$PNG_SO" -lm
+
+# Ambient-occlusion reference: the reference's performAmbientOcclusionNative on a geometry fixture.
+gcc $CFLAGS -c "$HERE/ao_ref_main.c" -o "$OUT/obj/ao_ref_main.o"
+gcc -o "$OUT/ao_ref" "$OUT/obj/ao_ref_main.o" "$OUT/obj/photonmap.o" "$OUT/obj/geoSphere.o" $COMMON "$PNG_SO" -lm
 
 # Drop-in link check: the reference CLI against our C-ABI library (needs the product .so built).
 LIB="$REPO/flatmatch-global-illumination_amd/libflatmatch_gi.so"

@@ -57,6 +57,10 @@ def load():
         lib.fmo_rand.argtypes = [C.POINTER(C.c_uint32)]
         lib.fmo_finalize.restype = None
         lib.fmo_finalize.argtypes = [vp, i64, vp, vp]
+        lib.ao_oracle.restype = C.c_int
+        lib.ao_oracle.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int]
+        lib.ao_oracle_tree.restype = i64
+        lib.ao_oracle_tree.argtypes = [vp, C.c_int, vp, i64]
         _lib = lib
     return _lib
 
@@ -187,3 +191,29 @@ def ref_run_items(scene, source: int, is_window: int, rng_states, variant: str =
     if _ref.ref_run_items(_p(win), _p(walls), len(walls), scene.num_texels, is_window, _p(rs), len(rs), _p(out)) != 0:
         raise RuntimeError(_ref.ref_last_error().decode())
     return out
+
+
+def ambient_occlusion(scene, wall_begin: int = 0, wall_end: int | None = None, dirs=None, nthreads: int = 0):
+    """The reference's performAmbientOcclusionNative restated (ao_oracle.c) on walls [wall_begin,
+    wall_end): float32 [numTexels, 4] texels, zero except those walls' level-0 texels. `dirs` is the
+    direction table (default: oracle/geosphere.py level 4, the reference's geoSphere4)."""
+    import geosphere
+
+    lib = load()
+    walls = np.ascontiguousarray(scene.walls)
+    we = len(walls) if wall_end is None else wall_end
+    d = np.ascontiguousarray(geosphere.generate(4) if dirs is None else dirs, dtype=np.float32)
+    tex = np.zeros((scene.num_texels, 4), np.float32)
+    threads = nthreads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    lib.ao_oracle(_p(walls), len(walls), wall_begin, we, _p(d), len(d), _p(tex), threads)
+    return tex
+
+
+def ao_tree(scene) -> np.ndarray:
+    """The oracle's BSP tree in fmgi_ao_tree's encoding."""
+    lib = load()
+    walls = np.ascontiguousarray(scene.walls)
+    n = lib.ao_oracle_tree(_p(walls), len(walls), None, 0)
+    out = np.zeros(max(n, 1), np.int32)
+    lib.ao_oracle_tree(_p(walls), len(walls), _p(out), n)
+    return out[:n]
