@@ -123,6 +123,13 @@ def load() -> C.CDLL:
         return _lib
     if not os.path.exists(LIB_PATH):
         raise FmgiError(f"{LIB_PATH} is missing: build it with `make -C {PKG_DIR}` (no CPU fallback exists)")
+    # One HIP runtime per process: PyTorch-ROCm wheels bundle their own libamdhip64. Loaded first, it
+    # satisfies this library's libamdhip64 dependency too; loaded second, a process ends up with two
+    # runtimes that enumerate devices independently (observed: one of them then sees no GPU).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     lib = C.CDLL(LIB_PATH)
     vp, i32, i64, u64 = C.c_void_p, C.c_int32, C.c_int64, C.c_uint64
     sig = {

@@ -66,3 +66,12 @@ def libc():
     lib.srand(1)  # glibc: srand(1) == the unseeded state main.c runs with
     yield lib
     lib.srand(1)
+
+
+@pytest.fixture(scope="module")
+def torch_cuda():
+    import torch
+
+    if not torch.cuda.is_available():
+        pytest.fail("GPU tests need an MI355X (torch.cuda.is_available() is False)")
+    return torch

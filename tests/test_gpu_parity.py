@@ -20,13 +20,6 @@ pytestmark = pytest.mark.gpu
 KERNELS = [fmgi.KERNEL_EXACT, fmgi.KERNEL_FAST, fmgi.KERNEL_GRID]
 
 
-@pytest.fixture(scope="module")
-def torch_cuda():
-    import torch
-
-    if not torch.cuda.is_available():
-        pytest.fail("GPU tests need an MI355X (torch.cuda.is_available() is False)")
-    return torch
 
 
 @pytest.fixture(scope="module")
