@@ -27,6 +27,7 @@
 #include "../../include/flatmatch_gi.h"
 #include "fmgi_ao.h"
 #include "fmgi_geosphere.h"
+#include "fmgi_output.h"
 
 #define FMGI_API extern "C" __attribute__((visibility("default")))
 
@@ -293,6 +294,84 @@ done:
 }
 
 } // namespace
+
+namespace {
+
+int output_run(const fmgi_geometry *geo, int spa, int tint, fmgi_vec3 *texels_out, uint8_t *rgb_out) {
+    if (!geo || !texels_out || !rgb_out) return internal_set_err(FMGI_ERR_ARG, "fmgi_output_tiles: null argument");
+    if (geo->numWalls < 0 || geo->numTexels < 0 || (geo->numWalls && !geo->walls) ||
+        (geo->numTexels && !geo->texels) || spa < 0)
+        return internal_set_err(FMGI_ERR_ARG, "fmgi_output_tiles: bad geometry");
+    std::vector<OutWall> ow((size_t)std::max(geo->numWalls, 1));
+    int64_t tiles = 0;
+    for (int i = 0; i < geo->numWalls; i++) {
+        const fmgi_rect &r = geo->walls[i];
+        const int32_t *lm = r.lightmapSetup;
+        if (lm[1] < 1 || lm[2] < 1 || lm[0] < 0 || (int64_t)lm[0] + (int64_t)lm[1] * lm[2] > geo->numTexels)
+            return internal_set_err(FMGI_ERR_ARG, "fmgi_output_tiles: a wall's texels lie outside numTexels");
+        OutWall &w = ow[i];
+        memset(&w, 0, sizeof w);
+        w.first_tile = tiles;
+        w.s0 = lm[0];
+        w.floor = r.pos.s[2] == 0 && r.width.s[2] == 0 && r.height.s[2] == 0;
+        const int nt = lm[1] * lm[2];
+        /* main.c:71: getNumTiles(obj) / (getArea(obj) * numSamplesPerArea), then 0.35 * that in double */
+        const float area = length(f3of(r.width)) * length(f3of(r.height));
+        const float per = nt / (area * spa);
+        w.norm = (float)(0.35 * per);
+        tiles += nt;
+    }
+    if (texels_out != geo->texels) memcpy(texels_out, geo->texels, (size_t)geo->numTexels * sizeof(fmgi_vec3));
+    if (tiles == 0) return FMGI_OK;
+    int dev_count = 0;
+    if (hipGetDeviceCount(&dev_count) != hipSuccess || dev_count <= 0)
+        return internal_set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
+    int rc = FMGI_OK;
+    OutWall *d_walls = nullptr;
+    float *d_tex = nullptr;
+    uint8_t *d_rgb = nullptr;
+    OutArgs a;
+    memset(&a, 0, sizeof a);
+    {
+        const char *dv = getenv("FMGI_DEVICE");
+        AOCHK(hipSetDevice(dv ? atoi(dv) : 0));
+    }
+    AOCHK(hipMalloc(&d_walls, ow.size() * sizeof(OutWall)));
+    AOCHK(hipMemcpy(d_walls, ow.data(), ow.size() * sizeof(OutWall), hipMemcpyHostToDevice));
+    AOCHK(hipMalloc(&d_tex, (size_t)geo->numTexels * sizeof(fmgi_vec3)));
+    AOCHK(hipMemcpy(d_tex, texels_out, (size_t)geo->numTexels * sizeof(fmgi_vec3), hipMemcpyHostToDevice));
+    AOCHK(hipMalloc(&d_rgb, (size_t)tiles * 3));
+    a.walls = d_walls;
+    a.nwalls = geo->numWalls;
+    a.ntexels = tiles;
+    a.texels = d_tex;
+    a.rgb = d_rgb;
+    a.normalise = spa > 0;
+    a.tint_extra = tint != 0;
+    AOCHK(fmgi_launch_output(a, nullptr));
+    AOCHK(hipDeviceSynchronize());
+    AOCHK(hipMemcpy(texels_out, d_tex, (size_t)geo->numTexels * sizeof(fmgi_vec3), hipMemcpyDeviceToHost));
+    AOCHK(hipMemcpy(rgb_out, d_rgb, (size_t)tiles * 3, hipMemcpyDeviceToHost));
+done:
+    hipFree(d_walls);
+    hipFree(d_tex);
+    hipFree(d_rgb);
+    return rc;
+}
+
+} // namespace
+
+FMGI_API int64_t fmgi_output_tile_bytes(const fmgi_geometry *geo) {
+    if (!geo || (geo->numWalls && !geo->walls)) return internal_set_err(FMGI_ERR_ARG, "bad geometry");
+    int64_t n = 0;
+    for (int i = 0; i < geo->numWalls; i++) n += 3 * (int64_t)geo->walls[i].lightmapSetup[1] * geo->walls[i].lightmapSetup[2];
+    return n;
+}
+
+FMGI_API int fmgi_output_tiles(const fmgi_geometry *geo, int numSamplesPerArea, int tintExtra, fmgi_vec3 *texels_out,
+                               uint8_t *rgb_out) {
+    return output_run(geo, numSamplesPerArea, tintExtra, texels_out, rgb_out);
+}
 
 FMGI_API int fmgi_geosphere(int levels, float *xyz, int cap) {
     if (levels < 1 || levels > 6) return internal_set_err(FMGI_ERR_ARG, "fmgi_geosphere: levels must be 1..6");

@@ -274,3 +274,15 @@ def ao_tree(sc: Scene) -> np.ndarray:
     out = np.zeros(max(n, 1), np.int32)
     lib.fmgi_ao_tree(C.byref(g), _ptr(out), n)
     return out[:n]
+
+
+def output_tiles(sc: Scene, texels: np.ndarray, spa: int, tint_extra: int = 0):
+    """The output step on the GPU (fmgi_output_tiles): (normalised texels, RGB8 bytes of every tile)."""
+    lib = load()
+    tex = np.ascontiguousarray(texels, np.float32)
+    out = np.empty_like(tex)
+    g, keep = make_geometry(sc, tex)
+    n = lib.fmgi_output_tile_bytes(C.byref(g))
+    rgb = np.zeros(max(n, 1), np.uint8)
+    check(lib.fmgi_output_tiles(C.byref(g), spa, tint_extra, _ptr(out), _ptr(rgb)), "fmgi_output_tiles")
+    return out, rgb[:n]

@@ -44,6 +44,8 @@ EXPORTS = (
     "fmgi_ambient_occlusion",
     "fmgi_geosphere",
     "fmgi_ao_tree",
+    "fmgi_output_tiles",
+    "fmgi_output_tile_bytes",
 )
 
 KERNEL_EXACT = 0
@@ -160,6 +162,8 @@ def load() -> C.CDLL:
         "fmgi_ambient_occlusion": (C.c_int, [vp, C.c_int, C.c_int, vp]),
         "fmgi_geosphere": (C.c_int, [C.c_int, vp, C.c_int]),
         "fmgi_ao_tree": (i64, [vp, vp, i64]),
+        "fmgi_output_tiles": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
+        "fmgi_output_tile_bytes": (i64, [vp]),
         "fmgi_grid_copy": (C.c_int, [vp, vp, vp, vp, vp]),
         "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
         "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),

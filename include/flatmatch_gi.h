@@ -80,6 +80,17 @@ int fmgi_geosphere(int levels, float *xyz, int cap);
    encoding's length and copies at most `cap` ints. */
 int64_t fmgi_ao_tree(const fmgi_geometry *geo, int32_t *out, int64_t cap);
 
+/* ---- Output step: what main.c:66-95 does after the bake, minus the PNG encoding */
+/* Normalisation for the photon modes (main.c:66-79; numSamplesPerArea = 0 skips it, as the reference
+   does for AO/radiosity), then every wall's RGB8 tile as the reference's saveAs()/saveAs_core
+   (rectangle.c:295-345) builds it before write_png_file: tone map 1 - exp(-2 L), clamp, floor tint
+   (tintExtra: the second tint of the AO/native modes). texels_out = geo->texels normalised;
+   rgb_out = the walls' tiles concatenated in wall order, fmgi_output_tile_bytes(geo) bytes.
+   Byte-identical to the reference. Returns 0 or FMGI_ERR_*. */
+int fmgi_output_tiles(const fmgi_geometry *geo, int numSamplesPerArea, int tintExtra, fmgi_vec3 *texels_out,
+                      uint8_t *rgb_out);
+int64_t fmgi_output_tile_bytes(const fmgi_geometry *geo);
+
 /* ---- Build-defined device-resident API ---------------------------------------------------------- */
 enum {
     FMGI_OK = 0,

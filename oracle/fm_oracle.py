@@ -59,6 +59,8 @@ def load():
         lib.fmo_finalize.argtypes = [vp, i64, vp, vp]
         lib.ao_oracle.restype = C.c_int
         lib.ao_oracle.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int]
+        lib.out_oracle.restype = None
+        lib.out_oracle.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp]
         lib.ao_oracle_tree.restype = i64
         lib.ao_oracle_tree.argtypes = [vp, C.c_int, vp, i64]
         _lib = lib
@@ -217,3 +219,15 @@ def ao_tree(scene) -> np.ndarray:
     out = np.zeros(max(n, 1), np.int32)
     lib.ao_oracle_tree(_p(walls), len(walls), _p(out), n)
     return out[:n]
+
+
+def output_tiles(scene, texels: np.ndarray, spa: int, tint_extra: int):
+    """main.c:66-79 normalisation (spa > 0) + saveAs_core tone map / floor tint (out_oracle.c):
+    returns (normalised float32 [numTexels, 4] texels, uint8 RGB bytes of every wall's tile)."""
+    lib = load()
+    walls = np.ascontiguousarray(scene.walls)
+    tex = np.array(texels, dtype=np.float32, copy=True)
+    n = int(sum(int(w["lm"][1]) * int(w["lm"][2]) for w in walls))
+    rgb = np.zeros(3 * n, np.uint8)
+    lib.out_oracle(_p(walls), len(walls), _p(tex), spa, tint_extra, _p(rgb))
+    return tex, rgb
