@@ -838,7 +838,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_AUTO) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     if (kernel == FMGI_KERNEL_AUTO) kernel = c->auto_kernel;
     if (b == e) return FMGI_OK;
-    if (c->nrects == 0 || c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
+    if (c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
+    /* no walls: every photon escapes at its first scan (photonmap.cl:208), so nothing is deposited */
+    if (c->nrects == 0) return FMGI_OK;
     HIPCHK(hipSetDevice(c->device));
     BakeArgs a;
     memset(&a, 0, sizeof a);
@@ -1077,6 +1079,39 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
 /* ---- the drop-in entry points ----------------------------------------------------------------- */
 
 /*
+ * libc rand() is part of the drop-in contract (global_illumination_cl.c:251: one call per launch, and
+ * the caller sees exactly those calls). The HIP runtime's first device initialisation in a process
+ * draws from the same generator (observed on ROCm 7: one call inside the first hipStreamCreate /
+ * allocation). So the schedule is built, with its rand() calls, before any HIP call, and the state is
+ * snapshotted then and restored after the device work. glibc keeps the TYPE_3 state in a 128-byte
+ * array whose first word records the read position; setstate() re-reads it from there.
+ */
+struct RandGuard {
+    char *state = nullptr;
+    char saved[128];
+    bool ok = false;
+    void save() {
+#ifdef __GLIBC__
+        static char scratch[128];
+        state = initstate(1, scratch, sizeof scratch); /* records the position in state[0], switches away */
+        if (!state) return;
+        memcpy(saved, state, sizeof saved);
+        setstate(state); /* back to the caller's array and position */
+        ok = true;
+#endif
+    }
+    void restore() {
+#ifdef __GLIBC__
+        if (!ok) return;
+        static char scratch2[128];
+        initstate(1, scratch2, sizeof scratch2); /* leave the caller's array (its header is rewritten) */
+        memcpy(state, saved, sizeof saved);
+        setstate(state);
+#endif
+    }
+};
+
+/*
  * One bake of a reference Geometry on all GPUs of the node (FMGI_GPUS, default: every visible device,
  * at most 8). The reference launch schedule is built once (libc rand() consumed exactly as the
  * reference does, global_illumination_cl.c:251) and its flattened work items are split into equal
@@ -1085,6 +1120,10 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
  * FMGI_SHARDS (tests only) splits into more shards than GPUs, round-robin, to exercise the reduction on
  * a single device.
  */
+static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int kernel,
+                                 const std::vector<int32_t> &offs, uint64_t items, fmgi_vec3 *texels_out,
+                                 bool verbose);
+
 static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_out, bool verbose) {
     if (!geo) return set_err(FMGI_ERR_ARG, "null geometry");
     const char *wg_env = getenv("FMGI_WG");
@@ -1095,6 +1134,30 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     if (k_env && !strcmp(k_env, "grid")) kernel = FMGI_KERNEL_GRID;
     if (k_env && !strcmp(k_env, "exact")) kernel = FMGI_KERNEL_EXACT;
     if (k_env && !strcmp(k_env, "fast")) kernel = FMGI_KERNEL_FAST;
+    /* the reference schedule and its rand() calls first, before the HIP runtime can draw from rand() */
+    std::vector<int32_t> offs;
+    uint64_t items = 0;
+    int64_t nl = 0;
+    {
+        fmgi_context *h = fmgi_create(FMGI_HOST_ONLY);
+        int rc0 = fmgi_set_scene(h, geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
+                                 geo->numLights, geo->numTexels);
+        if (rc0 == FMGI_OK) nl = fmgi_plan(h, spa, wg, nullptr, 0, &items);
+        if (rc0 == FMGI_OK && nl >= 0)
+            for (const LaunchDev &L : h->h_launches) offs.push_back(L.rng_offset);
+        fmgi_destroy(h);
+        if (rc0 != FMGI_OK) return rc0;
+        if (nl < 0) return (int)nl;
+    }
+    RandGuard guard;
+    guard.save();
+    const int rc_all = bake_geometry_devices(geo, spa, wg, kernel, offs, items, texels_out, verbose);
+    guard.restore();
+    return rc_all;
+}
+
+static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int kernel, const std::vector<int32_t> &offs,
+                                 uint64_t items, fmgi_vec3 *texels_out, bool verbose) {
     int ndev = fmgi_device_count();
     if (ndev <= 0) return set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
     const char *g_env = getenv("FMGI_GPUS");
@@ -1107,7 +1170,6 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     std::vector<void *> lm((size_t)nshard, nullptr);
     void *d_tex = nullptr, *d_stage = nullptr;
     size_t tb = (size_t)geo->numTexels * 16;
-    uint64_t items = 0;
     int rc = FMGI_OK;
     for (int k = 0; k < nshard && rc == FMGI_OK; k++) {
         ctx[k] = fmgi_create(k % ngpu);
@@ -1115,14 +1177,8 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
         rc = fmgi_set_scene(ctx[k], geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
                             geo->numLights, geo->numTexels);
         if (rc != FMGI_OK) break;
-        int64_t nl;
-        if (k == 0) {
-            nl = fmgi_plan(ctx[0], spa, wg, nullptr, 0, &items); /* the one rand() sequence */
-        } else {
-            std::vector<int32_t> offs;
-            for (const LaunchDev &L : ctx[0]->h_launches) offs.push_back(L.rng_offset);
-            nl = fmgi_plan(ctx[k], spa, wg, offs.data(), (int64_t)offs.size(), nullptr);
-        }
+        /* every shard replays the schedule planned above (the rand() values in offs) */
+        const int64_t nl = fmgi_plan(ctx[k], spa, wg, offs.data(), (int64_t)offs.size(), nullptr);
         if (nl < 0) rc = (int)nl;
         else if (k == 0 && verbose) {
             hipDeviceProp_t prop;

@@ -115,7 +115,7 @@ def bake(scene, launches: np.ndarray, item_begin: int = 0, item_end: int | None 
     """Exact fixed-point lightmap (int64 [numTexels, 3], units of 2^-25) of items [begin, end)."""
     lib = load()
     if item_end is None:
-        item_end = int(launches["item_begin"][-1] + launches["count"][-1])
+        item_end = int(launches["item_begin"][-1] + launches["count"][-1]) if len(launches) else 0
     walls = np.ascontiguousarray(scene.walls)
     src = np.ascontiguousarray(scene.sources)
     L = np.ascontiguousarray(launches, LAUNCH_DTYPE)
