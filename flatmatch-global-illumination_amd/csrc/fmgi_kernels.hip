@@ -278,6 +278,68 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
     }
 }
 
+/*
+ * Phase 1 of ScanGrid for scenes with at most 4 plane slots (the closed boxes: one plane per axis),
+ * nearest plane first. A plane contributes keys only at its own fac' f_p (every record on it shares
+ * f_p), so the planes are visited in increasing f_p and the visit stops at the first plane with
+ * f_p > L1 * (1 + 2^-11). Why that cannot change the scan's result: every skipped key exceeds
+ * L1 (1 + 2^-11) > f (1 + 2^-12) for the winner's exact fac f (|f - L1| <= 2^-20 L1), so
+ *   - the winner is not among them (L1 only decreases), and
+ *   - the separation test `L2 > f (1 + 2^-12)` has the same outcome with or without them.
+ * In a box the nearest facing plane holds the hit, so one cell lookup per scan instead of three.
+ */
+__device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
+                                                   float &L2, int &code1, unsigned &ntest) {
+    const int J0 = a.fJ[0], J01 = a.fJ[0] + a.fJ[1], JT = J01 + a.fJ[2];
+    const float rx = __builtin_amdgcn_rcpf(d.x), ry = __builtin_amdgcn_rcpf(d.y), rz = __builtin_amdgcn_rcpf(d.z);
+    float fk[4];
+    int qk[4];
+#pragma unroll
+    for (int k = 0; k < 4; k++) { /* fac' of every slot's facing plane: 1 LDS read + 2 VALU */
+        const int q = k < JT ? k : 0;
+        const bool ax0 = q < J0, ax1 = !ax0 && q < J01;
+        const float sa = ax0 ? s.x : (ax1 ? s.y : s.z), da = ax0 ? d.x : (ax1 ? d.y : d.z);
+        const float rd = ax0 ? rx : (ax1 ? ry : rz);
+        const float plane = *(const float *)(img + 96 * q + (da < 0.0f ? 0 : 48));
+        const float f = (plane - sa) * rd;
+        fk[k] = (k < JT && f >= 0.0f) ? f : INFINITY; /* behind, NaN or padding: no candidate */
+        qk[k] = q;
+    }
+    /* sort the 4 (f, slot) pairs ascending: 5 compare-exchanges */
+#define FMGI_CX(i, j)                                                                                  \
+    {                                                                                                  \
+        const bool sw = fk[j] < fk[i];                                                                 \
+        const float tf = sw ? fk[j] : fk[i];                                                           \
+        fk[j] = sw ? fk[i] : fk[j];                                                                    \
+        fk[i] = tf;                                                                                    \
+        const int tq = sw ? qk[j] : qk[i];                                                             \
+        qk[j] = sw ? qk[i] : qk[j];                                                                    \
+        qk[i] = tq;                                                                                    \
+    }
+    FMGI_CX(0, 1) FMGI_CX(2, 3) FMGI_CX(0, 2) FMGI_CX(1, 3) FMGI_CX(1, 2)
+#undef FMGI_CX
+    const uint2 *cells = (const uint2 *)a.gcells;
+    const float4 *recs = (const float4 *)a.grecs;
+    for (int k = 0; k < 4; k++) {
+        const float f = fk[k];
+        if (!(f < INFINITY) || f > L1 * 1.00048828125f) break; /* 1 + 2^-11 */
+        const int q = qk[k];
+        const bool ax0 = q < J0, ax1 = !ax0 && q < J01;
+        const float da = ax0 ? d.x : (ax1 ? d.y : d.z);
+        const float su = ax0 ? s.y : s.x, sv = (ax0 || ax1) ? s.z : s.y;
+        const float du = ax0 ? d.y : d.x, dv = (ax0 || ax1) ? d.z : d.y;
+        const float4 *p = (const float4 *)__builtin_assume_aligned(img + 96 * q + (da < 0.0f ? 0 : 48), 16);
+        const float4 g0 = p[0], g1 = p[1], g2 = p[2];
+        const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
+        const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
+        const float4 r0 = recs[c.y > 0 ? c.x : 0], r1 = recs[c.y > 1 ? c.x + 1 : 0];
+        ntest += c.y;
+        if (c.y > 0) grid_rec(f, uh, vh, r0, (int)c.x, L1, L2, code1);
+        if (c.y > 1) grid_rec(f, uh, vh, r1, (int)c.x + 1, L1, L2, code1);
+        for (uint32_t j = 2; j < c.y; j++) grid_rec(f, uh, vh, recs[c.x + j], (int)(c.x + j), L1, L2, code1);
+    }
+}
+
 /* calls fn(idx) for the rect index of every record that passes grid_axis's candidate test */
 template <int A, class F>
 __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, int J, f3 s, f3 d, F &&fn) {
@@ -345,9 +407,13 @@ struct ScanGrid {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         unsigned ntest = 0;
-        grid_axis<0>(a, lds, a.fJ[0], src, dir, L1, L2, code1, ntest);
-        grid_axis<1>(a, lds + 96 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
-        grid_axis<2>(a, lds + 96 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
+        if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
+            grid_phase1_sorted(a, lds, src, dir, L1, L2, code1, ntest);
+        } else {
+            grid_axis<0>(a, lds, a.fJ[0], src, dir, L1, L2, code1, ntest);
+            grid_axis<1>(a, lds + 96 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
+            grid_axis<2>(a, lds + 96 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
+        }
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;
         for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
