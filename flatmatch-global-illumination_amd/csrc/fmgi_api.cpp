@@ -335,6 +335,12 @@ GridBuild build_grid(const FilterBuild &fb) {
                 }
                 planes[a][c].push_back(g);
             }
+            /* nearest first along the lanes that face this class: the +a class (c = 0) is faced by rays
+               going -a, so its planes run by descending coordinate, the -a class by ascending; fac' is
+               then non-decreasing along a lane's walk and ScanGrid can stop early */
+            std::stable_sort(planes[a][c].begin(), planes[a][c].end(), [c](const GridPlane &x, const GridPlane &y) {
+                return c == 0 ? x.plane > y.plane : x.plane < y.plane;
+            });
         }
     }
     GridPlane pad;

@@ -268,6 +268,9 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
         const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
         const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue; /* plane behind the photon (or NaN): no candidate on it */
+        /* the host orders each class nearest-first, so fac' never decreases from here on: past the
+           2^-11 band above L1 no later plane can win or decide the separation (grid_phase1_sorted) */
+        if (f > L1 * 1.00048828125f) break;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
         const float4 r0 = recs[c.y > 0 ? c.x : 0], r1 = recs[c.y > 1 ? c.x + 1 : 0];
