@@ -220,14 +220,14 @@ hipError_t upload(T **dst, const std::vector<T> &v) {
 struct GridBuild {
     std::vector<GridPlane> img; /* per axis a: J[a] pairs {+a plane j, -a plane j} */
     int J[3] = {0, 0, 0};
-    std::vector<uint32_t> cells; /* {start, count} pairs */
-    std::vector<float> recs;     /* {cu, hwu, cv, hwv} per cell entry */
+    std::vector<GridCell> cells;
+    std::vector<float> recs; /* overflow records {cu, hwu, cv, hwv} (cell entries 2..count) */
     std::vector<int32_t> idx;
 };
 
 GridBuild build_grid(const FilterBuild &fb) {
     GridBuild gb;
-    gb.cells = {0u, 0u};
+    gb.cells.push_back(GridCell{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0, -1, -1, 0}); /* cell 0: empty */
     std::vector<GridPlane> planes[3][2];
     for (int a = 0; a < 3; a++) {
         for (int c = 0; c < 2; c++) {
@@ -315,7 +315,7 @@ GridBuild build_grid(const FilterBuild &fb) {
                 g.nv = nv;
                 g.mu = (float)(nu - 1);
                 g.mv = (float)(nv - 1);
-                g.cell_off = (int32_t)(gb.cells.size() / 2);
+                g.cell_off = (int32_t)gb.cells.size();
                 const double su = AU.slack, sv = AV.slack;
                 std::vector<std::vector<const FilterRec *>> bucket((size_t)nu * nv);
                 for (const FilterRec *r : R) {
@@ -326,12 +326,21 @@ GridBuild build_grid(const FilterBuild &fb) {
                         for (int iu = u0; iu <= u1; iu++) bucket[(size_t)iv * nu + iu].push_back(r);
                 }
                 for (const auto &b : bucket) {
-                    gb.cells.push_back((uint32_t)gb.idx.size());
-                    gb.cells.push_back((uint32_t)b.size());
-                    for (const FilterRec *r : b) {
-                        gb.recs.insert(gb.recs.end(), {r->cu, r->hwu, r->cv, r->hwv});
-                        gb.idx.push_back(r->idx);
+                    GridCell gc{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, (int32_t)b.size(), -1, -1,
+                                (int32_t)gb.idx.size()};
+                    if (b.size() > 0) {
+                        gc.cu0 = b[0]->cu, gc.hwu0 = b[0]->hwu, gc.cv0 = b[0]->cv, gc.hwv0 = b[0]->hwv;
+                        gc.idx0 = b[0]->idx;
                     }
+                    if (b.size() > 1) {
+                        gc.cu1 = b[1]->cu, gc.hwu1 = b[1]->hwu, gc.cv1 = b[1]->cv, gc.hwv1 = b[1]->hwv;
+                        gc.idx1 = b[1]->idx;
+                    }
+                    for (size_t k = 2; k < b.size(); k++) {
+                        gb.recs.insert(gb.recs.end(), {b[k]->cu, b[k]->hwu, b[k]->cv, b[k]->hwv});
+                        gb.idx.push_back(b[k]->idx);
+                    }
+                    gb.cells.push_back(gc);
                 }
                 planes[a][c].push_back(g);
             }
@@ -416,7 +425,7 @@ struct fmgi_context {
     GridPlane *d_gimg = nullptr;
     int gimg_bytes = 0;
     int gJ[3] = {0, 0, 0};
-    uint32_t *d_gcells = nullptr;
+    GridCell *d_gcells = nullptr;
     float *d_grecs = nullptr;
     int32_t *d_gidx = nullptr;
     int grid_cells = 0, grid_entries = 0;
@@ -636,7 +645,7 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     GridBuild gb = build_grid(fb);
     for (int a = 0; a < 3; a++) c->gJ[a] = gb.J[a];
     c->gimg_bytes = (int)(gb.img.size() * sizeof(GridPlane));
-    c->grid_cells = (int)(gb.cells.size() / 2);
+    c->grid_cells = (int)gb.cells.size();
     c->grid_entries = (int)gb.idx.size();
     c->h_grid = gb;
     {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
@@ -987,16 +996,16 @@ FMGI_API int fmgi_get_stage_cycles(fmgi_context *c, uint64_t out[16]) {
 FMGI_API int fmgi_grid_sizes(const fmgi_context *c, int32_t sizes[5]) {
     if (!c || !sizes) return set_err(FMGI_ERR_ARG, "fmgi_grid_sizes: bad arguments");
     for (int a = 0; a < 3; a++) sizes[a] = c->h_grid.J[a];
-    sizes[3] = (int32_t)(c->h_grid.cells.size() / 2);
+    sizes[3] = (int32_t)c->h_grid.cells.size();
     sizes[4] = (int32_t)c->h_grid.idx.size();
     return FMGI_OK;
 }
 
-FMGI_API int fmgi_grid_copy(const fmgi_context *c, void *planes, uint32_t *cells, float *recs, int32_t *idx) {
+FMGI_API int fmgi_grid_copy(const fmgi_context *c, void *planes, void *cells, float *recs, int32_t *idx) {
     if (!c) return set_err(FMGI_ERR_ARG, "fmgi_grid_copy: null context");
     const GridBuild &g = c->h_grid;
     if (planes) memcpy(planes, g.img.data(), g.img.size() * sizeof(GridPlane));
-    if (cells) memcpy(cells, g.cells.data(), g.cells.size() * sizeof(uint32_t));
+    if (cells) memcpy(cells, g.cells.data(), g.cells.size() * sizeof(GridCell));
     if (recs) memcpy(recs, g.recs.data(), g.recs.size() * sizeof(float));
     if (idx) memcpy(idx, g.idx.data(), g.idx.size() * sizeof(int32_t));
     return FMGI_OK;

@@ -31,6 +31,17 @@ struct GridPlane {
 };
 static_assert(sizeof(GridPlane) == 48, "GridPlane must be 48 B");
 
+/* One grid cell (48 B): its first two records inline {cu, hwu, cv, hwv} with their rect indices, so a
+   lookup in a cell of <= 2 records is one load and needs no index load; records 3..count live in the
+   overflow arrays at [rest, rest + count - 2). An absent inline record is {0, -1, 0, -1} (never a
+   candidate). */
+struct GridCell {
+    float cu0, hwu0, cv0, hwv0;
+    float cu1, hwu1, cv1, hwv1;
+    int32_t count, idx0, idx1, rest;
+};
+static_assert(sizeof(GridCell) == 48, "GridCell must be 48 B");
+
 struct BakeArgs {
     const RectDev *rects;
     int nrects;
@@ -55,9 +66,9 @@ struct BakeArgs {
     const int32_t *general;
     int ngeneral;
     /* grid kernel (ScanGrid): fimg/fJ then hold GridPlane pairs {+a plane j, -a plane j}; the cells
-       ({start, count} u32 pairs), the per-cell records (float4 {cu, hwu, cv, hwv}) and their rect
-       indices live in global memory */
-    const uint32_t *gcells;
+       (GridCell), the overflow records (float4 {cu, hwu, cv, hwv}) and their rect indices live in
+       global memory */
+    const void *gcells;
     const float *grecs;
     const int32_t *gridx;
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */

@@ -247,6 +247,20 @@ __device__ __forceinline__ void grid_rec(float f, float uh, float vh, float4 r, 
     L1 = lt ? key : L1;
 }
 
+/* the candidate tests of one cell: its two inline records (absent ones are never candidates), then its
+   overflow records (rare); code1 receives the winner's rect index */
+__device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const GridCell &c, float f, float uh, float vh,
+                                                float &L1, float &L2, int &code1, unsigned &ntest) {
+    ntest += (unsigned)c.count;
+    grid_rec(f, uh, vh, make_float4(c.cu0, c.hwu0, c.cv0, c.hwv0), c.idx0, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(c.cu1, c.hwu1, c.cv1, c.hwv1), c.idx1, L1, L2, code1);
+    if (c.count > 2) {
+        const float4 *recs = (const float4 *)a.grecs;
+        for (int k = 2; k < c.count; k++)
+            grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2], L1, L2, code1);
+    }
+}
+
 /*
  * Phase 1 of ScanGrid on the planes of axis A: per facing plane, fac' and the hit point once, the cell
  * it falls in, and the records of that cell (the first two loaded together with no wait in between).
@@ -262,8 +276,7 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
-    const uint2 *cells = (const uint2 *)a.gcells;
-    const float4 *recs = (const float4 *)a.grecs;
+    const GridCell *cells = (const GridCell *)a.gcells;
     for (int j = 0; j < J; j++) {
         const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
         const float f = (g0.x - sa) * rd;
@@ -272,12 +285,7 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
            2^-11 band above L1 no later plane can win or decide the separation (grid_phase1_sorted) */
         if (f > L1 * 1.00048828125f) break;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
-        const float4 r0 = recs[c.y > 0 ? c.x : 0], r1 = recs[c.y > 1 ? c.x + 1 : 0];
-        ntest += c.y;
-        if (c.y > 0) grid_rec(f, uh, vh, r0, (int)c.x, L1, L2, code1);
-        if (c.y > 1) grid_rec(f, uh, vh, r1, (int)c.x + 1, L1, L2, code1);
-        for (uint32_t k = 2; k < c.y; k++) grid_rec(f, uh, vh, recs[c.x + k], (int)(c.x + k), L1, L2, code1);
+        grid_cell_tests(a, cells[grid_cell(g0, g1, g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
     }
 }
 
@@ -321,8 +329,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
     }
     FMGI_CX(0, 1) FMGI_CX(2, 3) FMGI_CX(0, 2) FMGI_CX(1, 3) FMGI_CX(1, 2)
 #undef FMGI_CX
-    const uint2 *cells = (const uint2 *)a.gcells;
-    const float4 *recs = (const float4 *)a.grecs;
+    const GridCell *cells = (const GridCell *)a.gcells;
     for (int k = 0; k < 4; k++) {
         const float f = fk[k];
         if (!(f < INFINITY) || f > L1 * 1.00048828125f) break; /* 1 + 2^-11 */
@@ -334,12 +341,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const float4 *p = (const float4 *)__builtin_assume_aligned(img + 96 * q + (da < 0.0f ? 0 : 48), 16);
         const float4 g0 = p[0], g1 = p[1], g2 = p[2];
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
-        const float4 r0 = recs[c.y > 0 ? c.x : 0], r1 = recs[c.y > 1 ? c.x + 1 : 0];
-        ntest += c.y;
-        if (c.y > 0) grid_rec(f, uh, vh, r0, (int)c.x, L1, L2, code1);
-        if (c.y > 1) grid_rec(f, uh, vh, r1, (int)c.x + 1, L1, L2, code1);
-        for (uint32_t j = 2; j < c.y; j++) grid_rec(f, uh, vh, recs[c.x + j], (int)(c.x + j), L1, L2, code1);
+        grid_cell_tests(a, cells[grid_cell(g0, g1, g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
     }
 }
 
@@ -352,17 +354,19 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, i
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
-    const uint2 *cells = (const uint2 *)a.gcells;
+    const GridCell *cells = (const GridCell *)a.gcells;
     const float4 *recs = (const float4 *)a.grecs;
     for (int j = 0; j < J; j++) {
         const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
         const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        const uint2 c = cells[grid_cell(g0, g1, g2, uh, vh)];
-        for (uint32_t k = 0; k < c.y; k++) {
-            const float4 r = recs[c.x + k];
-            if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[c.x + k]);
+        const GridCell c = cells[grid_cell(g0, g1, g2, uh, vh)];
+        if (c.count > 0 && (int)(fabsf(uh - c.cu0) <= c.hwu0) & (int)(fabsf(vh - c.cv0) <= c.hwv0)) fn(c.idx0);
+        if (c.count > 1 && (int)(fabsf(uh - c.cu1) <= c.hwu1) & (int)(fabsf(vh - c.cv1) <= c.hwv1)) fn(c.idx1);
+        for (int k = 2; k < c.count; k++) {
+            const float4 r = recs[c.rest + k - 2];
+            if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[c.rest + k - 2]);
         }
     }
 }
@@ -424,7 +428,7 @@ struct ScanGrid {
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
             L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
-            code1 = lt ? -2 - g : code1;
+            code1 = lt ? G[g] : code1;
             L1 = lt ? key : L1;
         }
         st.tests += (unsigned long long)(ntest + (unsigned)a.ngeneral);
@@ -433,7 +437,7 @@ struct ScanGrid {
             best = INFINITY;
             return -1;
         }
-        const int idx = code1 >= 0 ? a.gridx[code1] : a.general[-2 - code1];
+        const int idx = code1; /* rect index of the phase-1 winner */
         const float f = exact_at(a.rects[idx], src, dir, INFINITY);
         const bool sep = !(f < 0) && L2 > f * 1.000244140625f; /* ScanFast's separation test */
         st.clk.lap(ST_SCAN2);

@@ -192,7 +192,7 @@ class Context:
         check(self.lib.fmgi_grid_sizes(self.h, _ptr(sz)), "fmgi_grid_sizes")
         npairs = int(sz[:3].sum())
         planes = np.zeros(2 * max(npairs, 1), GRID_PLANE_DTYPE)
-        cells = np.zeros((int(sz[3]), 2), np.uint32)
+        cells = np.zeros(int(sz[3]), GRID_CELL_DTYPE)
         recs = np.zeros((int(sz[4]), 4), np.float32)
         idx = np.zeros(int(sz[4]), np.int32)
         check(self.lib.fmgi_grid_copy(self.h, _ptr(planes), _ptr(cells), _ptr(recs), _ptr(idx)), "fmgi_grid_copy")
@@ -211,6 +211,9 @@ GRID_PLANE_DTYPE = np.dtype([("plane", "<f4"), ("u0", "<f4"), ("v0", "<f4"), ("i
                              ("mu", "<f4"), ("mv", "<f4"), ("nu", "<i4"), ("nv", "<i4"), ("cell_off", "<i4"),
                              ("pad0", "<i4"), ("pad1", "<i4")])
 assert GRID_PLANE_DTYPE.itemsize == 48
+GRID_CELL_DTYPE = np.dtype([("r0", "<f4", (4,)), ("r1", "<f4", (4,)), ("count", "<i4"), ("idx0", "<i4"),
+                            ("idx1", "<i4"), ("rest", "<i4")])
+assert GRID_CELL_DTYPE.itemsize == 48
 
 
 def make_geometry(sc: Scene, texels: np.ndarray):

@@ -212,19 +212,22 @@ int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, 
                      fmgi_event *events, int32_t *counts, uint32_t *rng_final);
 
 /* Grid tables of FMGI_KERNEL_GRID (built by fmgi_set_scene; host-only contexts too), for tests and
-   tooling. sizes[0..2] = plane pairs per axis (x, y, z), sizes[3] = cells, sizes[4] = cell entries.
+   tooling. sizes[0..2] = plane pairs per axis (x, y, z), sizes[3] = cells, sizes[4] = overflow entries.
    fmgi_grid_copy fills (any pointer may be NULL):
      planes[2 * (sizes[0] + sizes[1] + sizes[2])]: per axis, pairs {plane of the +n class, plane of the
        -n class}, each {float plane, u0, v0, iu, iv, mu, mv; int32 nu, nv, cell_off, pad[2]} (48 B;
        mu = nu - 1, mv = nv - 1; NaN plane = padding);
-     cells[2 * sizes[3]]: {first entry, count}; recs[4 * sizes[4]]: {cu, hwu, cv, hwv} (margin-grown
-     extents); idx[sizes[4]]: rect index. */
+     cells[sizes[3]] (48 B each): the cell's first two records {float cu, hwu, cv, hwv} (margin-grown
+       extents; {0, -1, 0, -1} when absent), then {int32 count, rect index of record 0, of record 1,
+       first overflow entry};
+     recs[4 * sizes[4]], idx[sizes[4]]: the overflow records (entries 3..count of every cell) and their
+       rect indices. */
 int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);
 /* Profiling builds only (make timing -> libflatmatch_gi_timing.so, -DFMGI_STAGE_TIMING): shader-clock
    cycles summed over waves per bake-loop stage {start, sample, scan phase 1, phase 2, fallback, hit,
    append}, since the last fmgi_reset_stats; all zero in the normal library. */
 int fmgi_get_stage_cycles(fmgi_context *ctx, uint64_t out[16]);
-int fmgi_grid_copy(const fmgi_context *ctx, void *planes, uint32_t *cells, float *recs, int32_t *idx);
+int fmgi_grid_copy(const fmgi_context *ctx, void *planes, void *cells, float *recs, int32_t *idx);
 
 /* Host helpers exported for tests (no device needed). */
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);

@@ -40,10 +40,19 @@ def _cell_of(p, u, v):
     return tv.astype(np.int64) * int(p["nu"]) + tu.astype(np.int64)
 
 
+def _entries(t, c):
+    """(records [n, 4], rect indices [n]) of one cell: the inline first record, then the overflow."""
+    n = int(c["count"])
+    inline = np.array([c["r0"], c["r1"]], np.float32)[: min(n, 2)]
+    ids = np.array([c["idx0"], c["idx1"]], np.int32)[: min(n, 2)]
+    rest = slice(int(c["rest"]), int(c["rest"]) + max(n - 2, 0))
+    return np.concatenate([inline, t["recs"][rest]]), np.concatenate([ids, t["idx"][rest]]).astype(np.int32)
+
+
 def _check_plane(t, p, cells, rng):
-    ent = np.unique(np.concatenate([np.arange(s, s + c) for s, c in cells if c] or [np.zeros(0, np.int64)]))
-    recs = t["recs"][ent]
-    ids = t["idx"][ent]
+    per_cell = [_entries(t, c) for c in cells]
+    recs = np.concatenate([r for r, _ in per_cell])
+    ids = np.concatenate([i for _, i in per_cell])
     # one record per rect of this plane (a rect's entries all carry the same extent)
     uniq, first = np.unique(ids, return_index=True)
     recs, ids = recs[first], uniq
@@ -72,7 +81,7 @@ def _check_plane(t, p, cells, rng):
     cell = _cell_of(p, U, V)
     # every record containing the point must be listed in the point's cell
     inside = (np.abs(U[:, None] - cu[None, :]) <= hwu[None, :]) & (np.abs(V[:, None] - cv[None, :]) <= hwv[None, :])
-    lists = [set(t["idx"][s : s + c].tolist()) for s, c in cells]
+    lists = [set(i.tolist()) for _, i in per_cell]
     missing = 0
     for k in np.nonzero(inside.any(axis=1))[0]:
         need = set(ids[inside[k]].tolist())
@@ -103,6 +112,6 @@ def test_grid_is_small_and_selective(box200, box2000):
         planes = _planes(t)
         assert len(planes) == 6  # a closed box: six planes
         tot = sum(len(c) for _, c in planes)
-        ent = sum(int(c[:, 1].sum()) for _, c in planes)
+        ent = sum(int(c["count"].sum()) for _, c in planes)
         assert tot <= 16 * len(sc.walls) + 16 * 6
         assert ent / tot < 2.0, ent / tot
