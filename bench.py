@@ -110,9 +110,16 @@ def main():
     local = int(os.environ.get("LOCAL_RANK", "0"))
     if world != args.gpus:
         raise SystemExit(f"--gpus {args.gpus} but WORLD_SIZE={world}")
-    torch.cuda.set_device(local)
+    # FMGI_BENCH_BACKEND=gloo rehearses the N-rank path on fewer GPUs (ranks share devices, reductions go
+    # through host memory); the default is RCCL, one rank per GPU
+    backend = os.environ.get("FMGI_BENCH_BACKEND", "nccl")
+    device_index = local % max(torch.cuda.device_count(), 1) if backend == "gloo" else local
+    torch.cuda.set_device(device_index)
     if world > 1:
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if backend == "nccl":
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        else:
+            dist.init_process_group(backend)
 
     cfg = dict(CONFIGS[args.config])
     if args.spa:
@@ -124,7 +131,7 @@ def main():
     kernel = {"auto": fmgi.KERNEL_AUTO, "grid": fmgi.KERNEL_GRID, "fast": fmgi.KERNEL_FAST,
               "exact": fmgi.KERNEL_EXACT}[args.kernel]
 
-    ctx = fmgi.Context(local)
+    ctx = fmgi.Context(device_index)
     ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE,
                           "stream": fmgi.ACCUM_STREAM, "none": fmgi.ACCUM_NONE}[args.accum])
     ctx.set_scene(sc)
@@ -134,7 +141,7 @@ def main():
     b, e = parallel.shard_range(total_items, rank, world)
     photons_per_step = 100 * total_items
 
-    dev = torch.device("cuda", local)
+    dev = torch.device("cuda", device_index)
     # one non-default stream for every device op of the step: the lightmap zero-fill, the bake kernel,
     # the RCCL reduce (ordered after it by torch) and the finalisation; HIP events time the bake on it
     stream = torch.cuda.Stream(device=dev)
@@ -185,9 +192,9 @@ def main():
     vals = torch.tensor([elapsed, st["scans"], st["deposits"], st["photons"]], dtype=torch.float64, device=dev)
     if world > 1:
         t_max = vals[:1].clone()
-        dist.all_reduce(t_max, op=dist.ReduceOp.MAX)
+        parallel.all_reduce(t_max, dist.ReduceOp.MAX)
         sums = vals[1:].clone()
-        dist.all_reduce(sums, op=dist.ReduceOp.SUM)
+        parallel.all_reduce(sums, dist.ReduceOp.SUM)
         elapsed = float(t_max.item())
         scans, deposits, photons_done = (float(x) for x in sums.tolist())
     else:
@@ -238,7 +245,8 @@ def main():
                 + (" (auto)" if kernel == fmgi.KERNEL_AUTO else ""),
                 "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)",
                                  4: "stream"}[ctx.accumulation],
-                "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)",
+                "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)" if backend == "nccl"
+                else f"dp{world} REHEARSAL ({backend}: ranks share {torch.cuda.device_count()} GPU(s), host reduce)",
             },
             "roofline": {
                 # BASELINE metric: achieved HBM GB/s of the dominant kernel (the bake), algorithmic bytes

@@ -18,10 +18,36 @@ def shard_range(total_items: int, rank: int, world: int) -> tuple[int, int]:
     return total_items * rank // world, total_items * (rank + 1) // world
 
 
+def _host_backend(group) -> bool:
+    import torch.distributed as dist
+
+    return dist.get_backend(group) == "gloo"
+
+
 def reduce_lightmap(lm, dst: int = 0, group=None):
-    """Sum the int64 [numTexels, 4] lightmaps of all ranks into rank `dst` (in place there)."""
+    """Sum the int64 [numTexels, 4] lightmaps of all ranks into rank `dst` (in place there). Device
+    tensors go through RCCL; with gloo (CPU tests, rehearsals) they are staged through host memory."""
     import torch.distributed as dist
 
     if dist.is_available() and dist.is_initialized() and dist.get_world_size(group) > 1:
-        dist.reduce(lm, dst=dst, op=dist.ReduceOp.SUM, group=group)
+        if lm.is_cuda and _host_backend(group):
+            host = lm.cpu()
+            dist.reduce(host, dst=dst, op=dist.ReduceOp.SUM, group=group)
+            if dist.get_rank(group) == dst:
+                lm.copy_(host)
+        else:
+            dist.reduce(lm, dst=dst, op=dist.ReduceOp.SUM, group=group)
     return lm
+
+
+def all_reduce(t, op, group=None):
+    """dist.all_reduce, staging device tensors through host memory on gloo."""
+    import torch.distributed as dist
+
+    if t.is_cuda and _host_backend(group):
+        host = t.cpu()
+        dist.all_reduce(host, op=op, group=group)
+        t.copy_(host)
+    else:
+        dist.all_reduce(t, op=op, group=group)
+    return t
