@@ -18,32 +18,11 @@
 
 #pragma clang fp contract(off)
 
+#include "fmgi_rect_dev.h"
+
 namespace {
 
-struct v3 {
-    float x, y, z;
-};
-__device__ __forceinline__ v3 mk(float x, float y, float z) { return v3{x, y, z}; }
-__device__ __forceinline__ v3 add(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); }
-__device__ __forceinline__ v3 sub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
-__device__ __forceinline__ v3 mul(v3 a, float f) { return mk(a.x * f, a.y * f, a.z * f); }
-__device__ __forceinline__ float dot(v3 a, v3 b) { return a.x * b.x + a.y * b.y + a.z * b.z; }
-
-/* rectangle.c:67-95 intersects(): -1 = no hit */
-__device__ __forceinline__ float ao_intersects(const AoRect &r, v3 src, v3 dir, float closest) {
-    const v3 n = mk(r.nx, r.ny, r.nz), pos = mk(r.px, r.py, r.pz);
-    const float denom = dot(n, dir);
-    if (denom >= 0) return -1;
-    const float fac = dot(n, sub(pos, src)) / denom;
-    if (fac < 0) return -1;
-    const v3 ray = mul(dir, fac);
-    if (closest * closest < dot(ray, ray)) return -1; /* squaredLength */
-    const v3 pdir = sub(add(src, ray), pos);
-    const float dx = dot(mk(r.wx, r.wy, r.wz), pdir);
-    const float dy = dot(mk(r.hx, r.hy, r.hz), pdir);
-    if (dx < 0 || dy < 0 || dx > r.wl || dy > r.hl) return -1;
-    return fac;
-}
+using namespace fmgi_dev;
 
 /* One stack frame of findClosestIntersection (photonmap.c:54-161). stage 0: test the node's items;
    stage 1: the nearer child (the side of the split plane the ray starts on) has returned `ret`;
@@ -66,7 +45,7 @@ __device__ int ao_find(const AoArgs &a, v3 pos0, v3 dir, float &dist) {
         const v3 ppos = mk(nd.px, nd.py, nd.pz), pn = mk(nd.nx, nd.ny, nd.nz);
         if (f.stage == 0) {
             for (int i = 0; i < nd.nitems; i++) { /* :70-82 */
-                const float dn = ao_intersects(a.items[nd.item0 + i], pos, dir, dist);
+                const float dn = rect_intersects(a.items[nd.item0 + i], pos, dir, dist);
                 if (dn == -1) continue;
                 if (dn + f.shift < dist) {
                     dist = dn + f.shift;

@@ -18,7 +18,7 @@ import ctypes as C
 import numpy as np
 
 from . import scene
-from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, Timing, FmgiError, Geometry, Stats,
+from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, RadStats, Timing, FmgiError, Geometry, Stats,
                    check, load)
 from .scene import RECT_DTYPE, Scene
 
@@ -253,6 +253,28 @@ def ambient_occlusion(sc: Scene, wall_begin: int = 0, wall_end: int | None = Non
     we = len(sc.walls) if wall_end is None else wall_end
     check(lib.fmgi_ambient_occlusion(C.byref(g), wall_begin, we, _ptr(out)), "fmgi_ambient_occlusion")
     return out
+
+
+def radiosity(sc: Scene, with_sids: bool = False):
+    """The reference's performRadiosityNative on the GPU (fmgi_radiosity): returns float32 [numTexels, 4]
+    texels, and with with_sids also the int32 [jobs, 10000] sourceTexelIds rows of the level-0 wall
+    texels. Consumes the process's libc rand() stream exactly as the reference does."""
+    lib = load()
+    tex = np.zeros((sc.num_texels, 4), np.float32)
+    out = np.empty_like(tex)
+    g, keep = make_geometry(sc, tex)
+    jobs = int(lib.fmgi_radiosity_jobs(C.byref(g)))
+    sids = np.zeros((jobs, 10000), np.int32) if with_sids else None
+    check(lib.fmgi_radiosity(C.byref(g), _ptr(out), _ptr(sids) if with_sids else None), "fmgi_radiosity")
+    return (out, sids) if with_sids else out
+
+
+def radiosity_stats() -> dict:
+    """fmgi_radiosity_stats: the last radiosity call's sizes and device phase times."""
+    lib = load()
+    st = RadStats()
+    check(lib.fmgi_radiosity_stats(C.byref(st)), "fmgi_radiosity_stats")
+    return st.as_dict()
 
 
 def geosphere(levels: int = 4) -> np.ndarray:

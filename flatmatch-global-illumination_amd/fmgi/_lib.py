@@ -46,6 +46,11 @@ EXPORTS = (
     "fmgi_ao_tree",
     "fmgi_output_tiles",
     "fmgi_output_tile_bytes",
+    "performRadiosityGpu",
+    "fmgi_radiosity",
+    "fmgi_radiosity_jobs",
+    "fmgi_radiosity_stats",
+    "fmgi_rand_skip",
 )
 
 KERNEL_EXACT = 0
@@ -86,6 +91,24 @@ class Timing(C.Structure):
         ("fold_ms", C.c_double),
         ("bake_launches", C.c_uint64),
         ("fold_launches", C.c_uint64),
+    ]
+
+    def as_dict(self):
+        return {k: (float if k.endswith("ms") else int)(getattr(self, k)) for k, _ in self._fields_}
+
+
+class RadStats(C.Structure):
+    """fmgi_rad_stats (include/flatmatch_gi.h)."""
+
+    _fields_ = [
+        ("jobs", C.c_int64),
+        ("rects", C.c_int64),
+        ("texels", C.c_int64),
+        ("rays", C.c_int64),
+        ("rand_ms", C.c_double),
+        ("rays_ms", C.c_double),
+        ("bounce_ms", C.c_double),
+        ("total_ms", C.c_double),
     ]
 
     def as_dict(self):
@@ -164,6 +187,11 @@ def load() -> C.CDLL:
         "fmgi_ao_tree": (i64, [vp, vp, i64]),
         "fmgi_output_tiles": (C.c_int, [vp, C.c_int, C.c_int, vp, vp]),
         "fmgi_output_tile_bytes": (i64, [vp]),
+        "performRadiosityGpu": (None, [vp]),
+        "fmgi_radiosity": (C.c_int, [vp, vp, vp]),
+        "fmgi_radiosity_jobs": (i64, [vp]),
+        "fmgi_radiosity_stats": (C.c_int, [C.POINTER(RadStats)]),
+        "fmgi_rand_skip": (C.c_int, [C.c_uint64]),
         "fmgi_grid_copy": (C.c_int, [vp, vp, vp, vp, vp]),
         "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
         "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),

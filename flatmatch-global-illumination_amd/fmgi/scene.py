@@ -151,12 +151,16 @@ def _grid(lo: float, hi: float, k: int):
     return [f32(lo + (hi - lo) * i / k) for i in range(k + 1)]
 
 
-def box_scene(n_rects: int = 200, room=(10.0, 8.0, 2.6)) -> Scene:
+def box_scene(n_rects: int = 200, room=(10.0, 8.0, 2.6), tile_size: float = TILE_SIZE,
+              with_light: bool = False) -> Scene:
     """Synthetic closed box: floor + ceiling tiled g x g, four walls tiled c x r,
     all normals inward, one 4 m x 1.45 m window (not in the rect list) on the y=0 wall.
 
     n_rects=200: floor 6x6, ceiling 6x6, walls 4 x (8 cols x 4 rows).
     n_rects=2000: floor 20x20, ceiling 20x20, walls 4 x (30 cols x 10 rows).
+    tile_size: lightmap texels per m² of the walls (the reference's TILE_SIZE, main.c:44); smaller
+    values give small test scenes. with_light adds a 0.5 m x 0.5 m ceiling light (1 x 1 texels, as
+    parseLayout.c:278-280 creates lights).
     """
     layouts = {200: (6, 8, 4), 2000: (20, 30, 10), 8: (1, 1, 1)}
     if n_rects not in layouts:
@@ -168,25 +172,30 @@ def box_scene(n_rects: int = 200, room=(10.0, 8.0, 2.6)) -> Scene:
     # floor (parseLayout.c:471 convention: pos at x_end, width -dx, height +dy -> n = +z)
     for j in range(g):
         for i in range(g):
-            walls.append(create_rectangle(xs[i + 1], ys[j], 0.0, f32(xs[i] - xs[i + 1]), 0, 0, 0, f32(ys[j + 1] - ys[j]), 0))
+            walls.append(create_rectangle(xs[i + 1], ys[j], 0.0, f32(xs[i] - xs[i + 1]), 0, 0, 0, f32(ys[j + 1] - ys[j]), 0,
+                                          tile_size))
     # ceiling (parseLayout.c:472: pos at x_start, width +dx, height +dy -> n = -z)
     zc = f32(Z)
     for j in range(g):
         for i in range(g):
-            walls.append(create_rectangle(xs[i], ys[j], zc, f32(xs[i + 1] - xs[i]), 0, 0, 0, f32(ys[j + 1] - ys[j]), 0))
+            walls.append(create_rectangle(xs[i], ys[j], zc, f32(xs[i + 1] - xs[i]), 0, 0, 0, f32(ys[j + 1] - ys[j]), 0,
+                                          tile_size))
     # walls: width (dx, dy, 0), height (0, 0, dz) -> n = normalized(-dy, dx, 0) (parseLayout.c:33-36)
     wx, wy = _grid(0.0, X, cols), _grid(0.0, Y, cols)
     for k in range(rows):
         dz = f32(zs[k + 1] - zs[k])
         for i in range(cols):
-            walls.append(create_rectangle(wx[i], 0.0, zs[k], f32(wx[i + 1] - wx[i]), 0, 0, 0, 0, dz))  # y=0, n=+y
-            walls.append(create_rectangle(wx[i + 1], f32(Y), zs[k], f32(wx[i] - wx[i + 1]), 0, 0, 0, 0, dz))  # y=Y, n=-y
-            walls.append(create_rectangle(0.0, wy[i + 1], zs[k], 0, f32(wy[i] - wy[i + 1]), 0, 0, 0, dz))  # x=0, n=+x
-            walls.append(create_rectangle(f32(X), wy[i], zs[k], 0, f32(wy[i + 1] - wy[i]), 0, 0, 0, dz))  # x=X, n=-x
+            walls.append(create_rectangle(wx[i], 0.0, zs[k], f32(wx[i + 1] - wx[i]), 0, 0, 0, 0, dz, tile_size))  # n=+y
+            walls.append(create_rectangle(wx[i + 1], f32(Y), zs[k], f32(wx[i] - wx[i + 1]), 0, 0, 0, 0, dz, tile_size))
+            walls.append(create_rectangle(0.0, wy[i + 1], zs[k], 0, f32(wy[i] - wy[i + 1]), 0, 0, 0, dz, tile_size))
+            walls.append(create_rectangle(f32(X), wy[i], zs[k], 0, f32(wy[i + 1] - wy[i]), 0, 0, 0, dz, tile_size))
     walls = np.array(walls, RECT_DTYPE)
     ntex = assign_texel_bases(walls)
     window = np.array([create_rectangle(3.0, 0.001, 0.85, 4.0, 0, 0, 0, 0, 1.45)], RECT_DTYPE)
-    return Scene(f"box{n_rects}", walls, window, np.zeros(0, RECT_DTYPE), ntex)
+    lights = (np.array([create_rectangle(5.0, 4.0, f32(Z - 0.001), 0.5, 0, 0, 0, 0.5, 0, 0.0)], RECT_DTYPE)
+              if with_light else np.zeros(0, RECT_DTYPE))
+    name = f"box{n_rects}" + ("" if tile_size == TILE_SIZE else f"_t{tile_size:g}") + ("_lit" if with_light else "")
+    return Scene(name, walls, window, lights, ntex)
 
 
 def spa_for_photons(scene: Scene, photons: float) -> int:

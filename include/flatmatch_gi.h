@@ -91,6 +91,34 @@ int fmgi_output_tiles(const fmgi_geometry *geo, int numSamplesPerArea, int tintE
                       uint8_t *rgb_out);
 int64_t fmgi_output_tile_bytes(const fmgi_geometry *geo);
 
+/* ---- Radiosity --------------------------------------------------------------- */
+/* The reference's performRadiosityNative (radiosityNative.h:10, radiosityNative.c:92-268) on the GPU:
+   10000 libc-rand() cosine rays per level-0 wall texel against its sorted candidate list, then 7
+   gather/update/mipmap bounces; geo->texels[0, numTexels) receive the result (w = 0). The caller's
+   libc rand() stream (glibc's default TYPE_3 generator) is replayed on the device and left where the
+   reference leaves it (2 x 10000 draws per level-0 wall texel). Same argument meaning and in-place
+   update; a different name so that the reference's radiosityNative.o can stay linked. Fatal errors
+   print "[Err] ..." and exit(-1). */
+void performRadiosityGpu(fmgi_geometry *geo);
+/* Non-mutating form: texels_out[numTexels] = the result; sids_out (NULL or jobs x 10000 int32) = the
+   reference's sourceTexelIds rows of the level-0 wall texels, wall/tile order (-1: the ray hit
+   nothing). Returns 0 or FMGI_ERR_*. */
+int fmgi_radiosity(const fmgi_geometry *geo, fmgi_vec3 *texels_out, int32_t *sids_out);
+/* number of level-0 wall texels (jobs); the rand() draws of a call are 20000 x this */
+int64_t fmgi_radiosity_jobs(const fmgi_geometry *geo);
+typedef struct fmgi_rad_stats {
+    int64_t jobs, rects, texels, rays; /* texels includes the window/light texels */
+    double rand_ms;                    /* device rand() replay */
+    double rays_ms;                    /* candidate lists + ray casts (+ uploads) */
+    double bounce_ms;                  /* 7 x (gather, update, mipmap) */
+    double total_ms;                   /* first upload .. last bounce */
+} fmgi_rad_stats;
+/* statistics of the last fmgi_radiosity / performRadiosityGpu call */
+int fmgi_radiosity_stats(fmgi_rad_stats *out);
+/* Host only: advance the caller's libc rand() generator by n draws with the jump matrices the
+   radiosity backend uses (as n rand() calls would). Returns 0 or FMGI_ERR_ARG (not glibc TYPE_3). */
+int fmgi_rand_skip(uint64_t n);
+
 /* ---- Build-defined device-resident API ---------------------------------------------------------- */
 enum {
     FMGI_OK = 0,

@@ -11,6 +11,8 @@
 #                                oracle/dump_geometry.c; turns a layout PNG into a geometry fixture.
 #   _ref/ao_ref                  reference photonmap.c/rectangle.c/vector3_cl.c/geoSphere.c + oracle/ao_ref_main.c:
 #                                performAmbientOcclusionNative on a geometry fixture (AO fixtures).
+#   _ref/rad_ref                 reference radiosityNative.o/rectangle.o/vector3_cl.o + oracle/rad_ref_main.c:
+#                                performRadiosityNative on a geometry fixture (radiosity fixtures).
 #   _ref/out_ref                 main.c:66-79 normalisation + the reference's saveAs()/read_png_file()
 #                                (output-step fixtures: RGB8 tile bytes).
 #   _ref/globalIllumination_fmgi reference main.c + its layout/IO objects linked against OUR
@@ -54,6 +56,10 @@ gcc -o "$OUT/dump_geometry" "$OUT/obj/dump_geometry.o" $COMMON "$PNG_SO" -lm
 # Ambient-occlusion reference: the reference's performAmbientOcclusionNative on a geometry fixture.
 gcc $CFLAGS -c "$HERE/ao_ref_main.c" -o "$OUT/obj/ao_ref_main.o"
 gcc -o "$OUT/ao_ref" "$OUT/obj/ao_ref_main.o" "$OUT/obj/photonmap.o" "$OUT/obj/geoSphere.o" $COMMON "$PNG_SO" -lm
+
+# Radiosity reference: the reference's performRadiosityNative on a geometry fixture, seeded rand().
+gcc $CFLAGS -c "$HERE/rad_ref_main.c" -o "$OUT/obj/rad_ref_main.o"
+gcc -o "$OUT/rad_ref" "$OUT/obj/rad_ref_main.o" "$OUT/obj/radiosityNative.o" $COMMON "$PNG_SO" -lm
 
 # Output-step reference: main.c:66-79 normalisation + the reference's saveAs() per wall, read back.
 gcc $CFLAGS -c "$HERE/out_ref_main.c" -o "$OUT/obj/out_ref_main.o"

@@ -61,6 +61,8 @@ def load():
         lib.ao_oracle.argtypes = [vp, C.c_int, C.c_int, C.c_int, vp, C.c_int, vp, C.c_int]
         lib.out_oracle.restype = None
         lib.out_oracle.argtypes = [vp, C.c_int, vp, C.c_int, C.c_int, vp]
+        lib.rad_oracle.restype = i64
+        lib.rad_oracle.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, C.c_int]
         lib.ao_oracle_tree.restype = i64
         lib.ao_oracle_tree.argtypes = [vp, C.c_int, vp, i64]
         _lib = lib
@@ -231,3 +233,24 @@ def output_tiles(scene, texels: np.ndarray, spa: int, tint_extra: int):
     rgb = np.zeros(3 * n, np.uint8)
     lib.out_oracle(_p(walls), len(walls), _p(tex), spa, tint_extra, _p(rgb))
     return tex, rgb
+
+
+RAD_RAYS = 10000  # geoSphereNumVectors, radiosityNative.c:151
+
+
+def radiosity(scene, nthreads: int = 0, with_sids: bool = False):
+    """The reference's performRadiosityNative restated (rad_oracle.c). Consumes libc rand() exactly as
+    the reference does (2 x 10000 values per level-0 wall texel), from the process's current state.
+    Returns float32 [numTexels, 4] texels, and with with_sids the int32 [jobs, 10000] sourceTexelIds rows
+    of the level-0 wall texels (wall/tile order)."""
+    lib = load()
+    walls, win, lights = (np.ascontiguousarray(a) for a in (scene.walls, scene.windows, scene.lights))
+    jobs = int(sum(int(w["lm"][1]) * int(w["lm"][2]) for w in walls))
+    tex = np.zeros((scene.num_texels, 4), np.float32)
+    sids = np.zeros((jobs, RAD_RAYS), np.int32) if with_sids else None
+    threads = nthreads or int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or (os.cpu_count() or 1)
+    n = lib.rad_oracle(_p(walls), len(walls), _p(win), len(win), _p(lights), len(lights), scene.num_texels,
+                       _p(tex), _p(sids) if with_sids else None, threads)
+    if n < 0:
+        raise MemoryError("rad_oracle: allocation failed")
+    return (tex, sids) if with_sids else tex

@@ -54,7 +54,8 @@ def test_no_symbol_clashes_with_reference_objects():
     exported = _exports()
     assert not (exported & clashing)
     extra = {s for s in exported if not s.startswith("fmgi_")}
-    assert extra == {"performGlobalIlluminationCl", "getGlobalIlluminationCl", "performAmbientOcclusionGpu"}
+    assert extra == {"performGlobalIlluminationCl", "getGlobalIlluminationCl", "performAmbientOcclusionGpu",
+                     "performRadiosityGpu"}
 
 
 def test_struct_layouts_match_reference_abi():

@@ -1,6 +1,8 @@
 #!/usr/bin/env bash
 # One gpurun session. Steps (FMGI_STEPS, space separated):
 #   tests            pytest -m gpu
+#   tests_k          pytest -m gpu $TESTS_ARGS (e.g. '-k radiosity')
+#   rad / radprof    tools/bench_rad.py $RAD_ARGS (plain / under rocprofv3 --kernel-trace --stats)
 #   ref              reference-kernel pin (tests/golden/make_ref_fixtures.py)
 #   bench            python bench.py $BENCH_ARGS
 #   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
@@ -25,6 +27,9 @@ export TMPDIR=/tmp
 for s in ${FMGI_STEPS:-tests ref bench prof}; do
   case $s in
     tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests_k) step tests_k 900 python -m pytest -m gpu -q -x -p no:cacheprovider ${TESTS_ARGS:-tests} ;;
+    rad)   step rad 900 python tools/bench_rad.py ${RAD_ARGS:-} ;;
+    radprof) step radprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/radprof" -o run --output-format csv -- python tools/bench_rad.py --reps 1 --no-cpu-baseline ${RAD_ARGS:-} ;;
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; step "$s" 600 python bench.py ${!v:-} ;;
