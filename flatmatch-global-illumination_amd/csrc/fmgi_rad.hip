@@ -188,6 +188,7 @@ __global__ __launch_bounds__(256) void k_rad_rays(RadArgs a) {
  * (a ray that hit nothing adds nothing). The order of the adds is the reference's; only the loads are
  * batched: GATHER_B source ids per block, the next block's ids in flight while the current block's
  * texels load, so a lane waits one memory round trip per block instead of two per ray.
+ * Random 16-B gathers from an L2-resident texel table: bound by cache lines per cycle per CU.
  */
 constexpr int GATHER_B = 25;
 static_assert(FMGI_RAD_RAYS % GATHER_B == 0, "gather blocks must tile the rays");
@@ -210,20 +211,15 @@ __global__ __launch_bounds__(256) void k_rad_gather(RadBounce b) {
             for (int i = 0; i < GATHER_B; i++)
                 nxt[i] = __builtin_nontemporal_load(s + (int64_t)(k0 + GATHER_B + i) * stride);
         }
-        float tx[GATHER_B], ty[GATHER_B], tz[GATHER_B];
+        float4 t[GATHER_B]; /* one 16-B load per ray: a random gather costs a cache line per lane */
 #pragma unroll
-        for (int i = 0; i < GATHER_B; i++) {
-            const float *p = (const float *)(b.src + (id[i] < 0 ? 0 : id[i]));
-            tx[i] = p[0];
-            ty[i] = p[1];
-            tz[i] = p[2];
-        }
+        for (int i = 0; i < GATHER_B; i++) t[i] = b.src[id[i] < 0 ? 0 : id[i]];
 #pragma unroll
         for (int i = 0; i < GATHER_B; i++) {
             const bool hit = id[i] >= 0;
-            x = hit ? x + tx[i] : x;
-            y = hit ? y + ty[i] : y;
-            z = hit ? z + tz[i] : z;
+            x = hit ? x + t[i].x : x;
+            y = hit ? y + t[i].y : y;
+            z = hit ? z + t[i].z : z;
         }
     }
     b.dest[b.jobs[job].texel] = make_float4(x, y, z, 0.0f);

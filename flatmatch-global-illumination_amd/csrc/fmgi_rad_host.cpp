@@ -399,6 +399,7 @@ int rad_run(const fmgi_geometry *geo, fmgi_vec3 *texels_out, int32_t *sids_out) 
     }
     {
         float ms = 0;
+        RADCHK(hipEventSynchronize(ev[3]));
         RADCHK(hipEventElapsedTime(&ms, ev[0], ev[1]));
         g_stats.rays_ms = ms - g_stats.rand_ms; /* rays + uploads */
         RADCHK(hipEventElapsedTime(&ms, ev[2], ev[3]));
