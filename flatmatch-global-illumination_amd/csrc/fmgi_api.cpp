@@ -606,7 +606,14 @@ static int ensure_stream(fmgi_context *c, uint64_t items, int grid, int block) {
     if (!c->sb.cursor) HIPCHK(hipMalloc(&c->sb.cursor, 64));
     c->sb.cap = cap;
     c->sb.colpack = c->d_colpack;
-    c->sb.groups = std::max(1, (2 * c->num_cus + P - 1) / P); /* ~2 sum workgroups per CU */
+    /* k_tile_runs runs one 112-KiB workgroup per CU at a time and tiles carry uneven code counts:
+       ~8 rounds of P x groups workgroups balance the tail (box200, 23 tiles: 28.4 ms fold at 89
+       groups vs 31.1 ms at 23 and 34.8 ms at 11; flat from ~33 groups up) */
+    {
+        const int ncu = std::max(1, c->num_cus);
+        const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
+        c->sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (8 * ncu + P - 1) / P);
+    }
     return FMGI_OK;
 }
 
