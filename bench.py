@@ -33,6 +33,9 @@ CONFIGS = {
                     desc="synthetic 2000-rectangle box scene, 1e9 photons per GPU (BASELINE config 5)"),
     "example": dict(scene="example", spa=6_500_000, weak=True,
                     desc="example.png layout, 1e8 photons per GPU (BASELINE config 2)"),
+    "apartment30": dict(scene="apartment30", spa=3_000_000, weak=True,
+                        desc="generated 30-room layout (654 walls, 34 light sources), 1.8e8 photons per GPU "
+                             "(not a BASELINE config: the acceleration structure on a large layout)"),
 }
 METRIC = "photons/sec + achieved HBM GB/s (% of peak), 200-rect scene, 1/2/4/8 MI355X"
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector == FP32 matrix peak on gfx950
@@ -42,8 +45,8 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 def load_scene(name):
     from fmgi import scene
 
-    if name == "example":
-        return scene.load_geometry(os.path.join(REPO, "tests", "golden", "example_geometry.bin"), "example")
+    if name in ("example", "apartment30"):
+        return scene.load_geometry(os.path.join(REPO, "tests", "golden", f"{name}_geometry.bin"), name)
     return scene.box_scene(int(name[3:]))
 
 

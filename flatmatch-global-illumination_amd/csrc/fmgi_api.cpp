@@ -316,6 +316,13 @@ GridBuild build_grid(const FilterBuild &fb) {
                 g.mu = (float)(nu - 1);
                 g.mv = (float)(nv - 1);
                 g.cell_off = (int32_t)gb.cells.size();
+                /* the records' box, widened by far more than the rounding of the kernel's float hit
+                   point and of |uh - cu| (so a point outside it fails every record test) */
+                const double pad_u = 1e-5 * (fabs(ulo) + fabs(uhi) + 1.0), pad_v = 1e-5 * (fabs(vlo) + fabs(vhi) + 1.0);
+                g.ulo = (float)(ulo - pad_u);
+                g.uhi = (float)(uhi + pad_u);
+                g.vlo = (float)(vlo - pad_v);
+                g.vhi = (float)(vhi + pad_v);
                 const double su = AU.slack, sv = AV.slack;
                 std::vector<std::vector<const FilterRec *>> bucket((size_t)nu * nv);
                 for (const FilterRec *r : R) {
@@ -358,6 +365,8 @@ GridBuild build_grid(const FilterBuild &fb) {
     pad.nu = pad.nv = 1;
     pad.mu = pad.mv = 0.0f;
     pad.cell_off = 0;
+    pad.ulo = pad.vlo = -INFINITY; /* never culled; fac' = NaN keeps it out anyway */
+    pad.uhi = pad.vhi = INFINITY;
     for (int a = 0; a < 3; a++) {
         gb.J[a] = (int)std::max(planes[a][0].size(), planes[a][1].size());
         for (int j = 0; j < gb.J[a]; j++)

@@ -27,9 +27,11 @@ struct GridPlane {
     float plane, u0, v0, iu; /* iu, iv = cells per unit length */
     float iv, mu, mv;        /* mu = nu - 1, mv = nv - 1 (the clamp bounds of the cell coordinates) */
     int32_t nu, nv, cell_off;
-    int32_t pad0, pad1;
+    float ulo, uhi, vlo, vhi; /* box of the plane's grown record extents, rounded outward: a hit point
+                                 outside it passes no record test, so its cell need not be loaded */
+    float pad0, pad1;
 };
-static_assert(sizeof(GridPlane) == 48, "GridPlane must be 48 B");
+static_assert(sizeof(GridPlane) == 64, "GridPlane must be 64 B");
 
 /* One grid cell (48 B): its first two records inline {cu, hwu, cv, hwv} with their rect indices, so a
    lookup in a cell of <= 2 records is one load and needs no index load; records 3..count live in the

@@ -228,7 +228,7 @@ struct ScanFast {
  * its separation argument carry over unchanged. A closed box of 200 rects has 6 planes: ~3 cells and a
  * few records per scan instead of ~100 rect tests.
  */
-/* The kernel's cell of hit point (uh, vh) on plane record g (48 B, see GridPlane). */
+/* The kernel's cell of hit point (uh, vh) on plane record g (64 B, see GridPlane). */
 __device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, const float4 g2, float uh, float vh) {
     /* g0 = {plane, u0, v0, iu}, g1 = {iv, mu, mv, nu}, g2 = {nv, cell_off, -, -} */
     const float tu = fminf(fmaxf((uh - g0.y) * g0.w, 0.0f), g1.y);
@@ -264,8 +264,11 @@ __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const GridCel
 /*
  * Phase 1 of ScanGrid on the planes of axis A: per facing plane, fac' and the hit point once, the cell
  * it falls in, and the records of that cell (the first two loaded together with no wait in between).
- * The LDS image holds, per axis, pairs {+A plane j, -A plane j} of 48-B GridPlane records; a lane reads
- * the one its direction faces.
+ * The LDS image holds, per axis, pairs {+A plane j, -A plane j} of 64-B GridPlane records; a lane reads
+ * the one its direction faces. Planes run nearest-first along the lane's direction, so the planes
+ * behind it are a prefix (fac' is monotone in the plane coordinate): a binary search skips them. A hit
+ * point outside the box of a plane's records passes none of their tests, so that plane's cell is not
+ * loaded.
  */
 template <int A>
 __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, int J, f3 s, f3 d, float &L1,
@@ -275,17 +278,25 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
-    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 64), 16);
     const GridCell *cells = (const GridCell *)a.gcells;
-    for (int j = 0; j < J; j++) {
-        const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
+    int lo = 0, hi = J; /* first plane not behind the photon (padding planes, fac' = NaN, count as not) */
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((p[8 * mid].x - sa) * rd < 0.0f) lo = mid + 1;
+        else hi = mid;
+    }
+    for (int j = lo; j < J; j++) {
+        const float4 g0 = p[8 * j];
         const float f = (g0.x - sa) * rd;
-        if (!(f >= 0.0f)) continue; /* plane behind the photon (or NaN): no candidate on it */
+        if (!(f >= 0.0f)) continue; /* padding plane (NaN) */
         /* the host orders each class nearest-first, so fac' never decreases from here on: past the
            2^-11 band above L1 no later plane can win or decide the separation (grid_phase1_sorted) */
         if (f > L1 * 1.00048828125f) break;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        grid_cell_tests(a, cells[grid_cell(g0, g1, g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
+        const float4 g2 = p[8 * j + 2], g3 = p[8 * j + 3];
+        if (uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y) continue;
+        grid_cell_tests(a, cells[grid_cell(g0, p[8 * j + 1], g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
     }
 }
 
@@ -311,7 +322,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const bool ax0 = q < J0, ax1 = !ax0 && q < J01;
         const float sa = ax0 ? s.x : (ax1 ? s.y : s.z), da = ax0 ? d.x : (ax1 ? d.y : d.z);
         const float rd = ax0 ? rx : (ax1 ? ry : rz);
-        const float plane = *(const float *)(img + 96 * q + (da < 0.0f ? 0 : 48));
+        const float plane = *(const float *)(img + 128 * q + (da < 0.0f ? 0 : 64));
         const float f = (plane - sa) * rd;
         fk[k] = (k < JT && f >= 0.0f) ? f : INFINITY; /* behind, NaN or padding: no candidate */
         qk[k] = q;
@@ -338,7 +349,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const float da = ax0 ? d.x : (ax1 ? d.y : d.z);
         const float su = ax0 ? s.y : s.x, sv = (ax0 || ax1) ? s.z : s.y;
         const float du = ax0 ? d.y : d.x, dv = (ax0 || ax1) ? d.z : d.y;
-        const float4 *p = (const float4 *)__builtin_assume_aligned(img + 96 * q + (da < 0.0f ? 0 : 48), 16);
+        const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * q + (da < 0.0f ? 0 : 64), 16);
         const float4 g0 = p[0], g1 = p[1], g2 = p[2];
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         grid_cell_tests(a, cells[grid_cell(g0, g1, g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
@@ -353,11 +364,11 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, i
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
-    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 64), 16);
     const GridCell *cells = (const GridCell *)a.gcells;
     const float4 *recs = (const float4 *)a.grecs;
     for (int j = 0; j < J; j++) {
-        const float4 g0 = p[6 * j], g1 = p[6 * j + 1], g2 = p[6 * j + 2];
+        const float4 g0 = p[8 * j], g1 = p[8 * j + 1], g2 = p[8 * j + 2];
         const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
@@ -389,8 +400,8 @@ struct ScanGrid {
             int nxt = INT_MAX;
             auto take = [&](int idx) { nxt = (idx > prev && idx < nxt) ? idx : nxt; };
             grid_visit<0>(a, lds, a.fJ[0], src, dir, take);
-            grid_visit<1>(a, lds + 96 * a.fJ[0], a.fJ[1], src, dir, take);
-            grid_visit<2>(a, lds + 96 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
+            grid_visit<1>(a, lds + 128 * a.fJ[0], a.fJ[1], src, dir, take);
+            grid_visit<2>(a, lds + 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
             for (int g = 0; g < a.ngeneral; g++) {
                 const int idx = a.general[g];
                 if (idx > prev && idx < nxt && exact_on(R, idx, src, dir, INFINITY) >= 0) nxt = idx;
@@ -417,9 +428,12 @@ struct ScanGrid {
         if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
             grid_phase1_sorted(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
+            /* floors and ceilings first: in a layout they bound almost every ray, and the x / y walks
+               stop at the first plane past L1 (the order of the axes changes neither L1 nor L2; an
+               exact tie of keys fails the separation test whatever the order) */
+            grid_axis<2>(a, lds + 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
             grid_axis<0>(a, lds, a.fJ[0], src, dir, L1, L2, code1, ntest);
-            grid_axis<1>(a, lds + 96 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
-            grid_axis<2>(a, lds + 96 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
+            grid_axis<1>(a, lds + 128 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
         }
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;

@@ -209,8 +209,9 @@ class Context:
 
 GRID_PLANE_DTYPE = np.dtype([("plane", "<f4"), ("u0", "<f4"), ("v0", "<f4"), ("iu", "<f4"), ("iv", "<f4"),
                              ("mu", "<f4"), ("mv", "<f4"), ("nu", "<i4"), ("nv", "<i4"), ("cell_off", "<i4"),
-                             ("pad0", "<i4"), ("pad1", "<i4")])
-assert GRID_PLANE_DTYPE.itemsize == 48
+                             ("ulo", "<f4"), ("uhi", "<f4"), ("vlo", "<f4"), ("vhi", "<f4"),
+                             ("pad0", "<f4"), ("pad1", "<f4")])
+assert GRID_PLANE_DTYPE.itemsize == 64
 GRID_CELL_DTYPE = np.dtype([("r0", "<f4", (4,)), ("r1", "<f4", (4,)), ("count", "<i4"), ("idx0", "<i4"),
                             ("idx1", "<i4"), ("rest", "<i4")])
 assert GRID_CELL_DTYPE.itemsize == 48

@@ -88,14 +88,38 @@ def _check_plane(t, p, cells, rng):
         if not need <= lists[cell[k]]:
             missing += 1
     assert missing == 0, f"{missing} points whose containing records are not in their cell"
+    # the plane's cull box (grid_axis skips the cell when the hit point is outside it): no point outside
+    # the box passes any record's float test |x - c| <= hw, so skipping cannot drop a candidate
+    f32 = np.float32
+    assert p["ulo"] < lo_u and p["uhi"] > hi_u and p["vlo"] < lo_v and p["vhi"] > hi_v
+    ob_u = np.concatenate([np.nextafter(f32(p["ulo"]), f32(-np.inf), dtype=np.float32) - rng.uniform(0, 1, 500).astype(f32),
+                           np.nextafter(f32(p["uhi"]), f32(np.inf), dtype=np.float32) + rng.uniform(0, 1, 500).astype(f32)])
+    ob_v = rng.uniform(lo_v, hi_v, 1000).astype(f32)
+    for Uo, Vo in ((ob_u, ob_v), (rng.uniform(lo_u, hi_u, 1000).astype(f32), ob_u - f32(p["ulo"]) + f32(p["vlo"]))):
+        ok = (np.abs(Uo[:, None] - cu[None, :]) <= hwu[None, :]) & (np.abs(Vo[:, None] - cv[None, :]) <= hwv[None, :])
+        outside = (Uo < f32(p["ulo"])) | (Uo > f32(p["uhi"])) | (Vo < f32(p["vlo"])) | (Vo > f32(p["vhi"]))
+        assert not (ok & outside[:, None]).any(), "a point outside the cull box passes a record test"
+    # just outside the box edges, at every record's centre line
+    for arr_u, arr_v in (([np.nextafter(f32(p["ulo"]), f32(-np.inf), dtype=np.float32)] * len(cv), cv),
+                         ([np.nextafter(f32(p["uhi"]), f32(np.inf), dtype=np.float32)] * len(cv), cv),
+                         (cu, [np.nextafter(f32(p["vlo"]), f32(-np.inf), dtype=np.float32)] * len(cu)),
+                         (cu, [np.nextafter(f32(p["vhi"]), f32(np.inf), dtype=np.float32)] * len(cu))):
+        Uo, Vo = np.asarray(arr_u, f32), np.asarray(arr_v, f32)
+        ok = (np.abs(Uo[:, None] - cu[None, :]) <= hwu[None, :]) & (np.abs(Vo[:, None] - cv[None, :]) <= hwv[None, :])
+        assert not ok.any()
     return len(ids)
 
 
-@pytest.mark.parametrize("name", ["example", "box200", "box2000", "box8"])
+@pytest.mark.parametrize("name", ["example", "box200", "box2000", "box8", "apartment30"])
 def test_grid_cells_cover_every_containing_record(name, example_scene, box200, box2000):
+    import os
+
+    from conftest import GOLDEN
     from fmgi import scene
 
-    sc = {"example": example_scene, "box200": box200, "box2000": box2000, "box8": scene.box_scene(8)}[name]
+    sc = {"example": lambda: example_scene, "box200": lambda: box200, "box2000": lambda: box2000,
+          "box8": lambda: scene.box_scene(8),
+          "apartment30": lambda: scene.load_geometry(os.path.join(GOLDEN, "apartment30_geometry.bin"), "a30")}[name]()
     t = _tables(sc)
     rng = np.random.default_rng(7)
     n = 0
