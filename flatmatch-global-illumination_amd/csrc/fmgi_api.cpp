@@ -897,6 +897,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.gcells = c->d_gcells;
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
+        a.grid_axes = (c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES")) ? 1 : 0;
     } else {
         a.fimg = c->d_fimg;
         a.fimg_bytes = c->fimg_bytes;

@@ -120,16 +120,36 @@ FMGI_HD float intersect_exact(f3 n, f3 pos, f3 wn, float wl, f3 hn, float hl, f3
     return fac;
 }
 
-/* photonmap.cl:95-120 */
-FMGI_HD int tile_at(f3 pos, f3 wn, float wl, f3 hn, float hl, int W, int H, f3 p) {
-    f3 pDir = sub3(p, pos);
-    float dx = dot3(wn, pDir);
-    float dy = dot3(hn, pDir);
+/* intersect_exact with closest = INFINITY (the early-out never fires), also returning the hit point's
+   dx = dot(wn, p - pos) and dy = dot(hn, p - pos): the same ops, in the same order, as tile_at's on the
+   point p = src + dir * fac that photonmap.cl:216 moves to, so the deposit needs no second evaluation */
+FMGI_HD float intersect_exact_uv(f3 n, f3 pos, f3 wn, float wl, f3 hn, float hl, f3 src, f3 dir, float &dx,
+                                 float &dy) {
+    float denom = dot3(n, dir);
+    if (denom >= 0) return -1;
+    float fac = dot3(n, sub3(pos, src)) / denom;
+    if (fac < 0) return -1;
+    f3 pDir = sub3(add3(src, mul3(dir, fac)), pos);
+    dx = dot3(wn, pDir);
+    if (dx < 0 || dx > wl) return -1;
+    dy = dot3(hn, pDir);
+    if (dy < 0 || dy > hl) return -1;
+    return fac;
+}
+
+/* photonmap.cl:108-119: the tile of in-rect coordinates (dx, dy) */
+FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, int W, int H) {
     int tx = (int)(dx * (float)W / wl);
     int ty = (int)(dy * (float)H / hl);
     tx = tx < 0 ? 0 : (tx > W - 1 ? W - 1 : tx);
     ty = ty < 0 ? 0 : (ty > H - 1 ? H - 1 : ty);
     return ty * W + tx;
+}
+
+/* photonmap.cl:95-120 */
+FMGI_HD int tile_at(f3 pos, f3 wn, float wl, f3 hn, float hl, int W, int H, f3 p) {
+    f3 pDir = sub3(p, pos);
+    return tile_uv(dot3(wn, pDir), dot3(hn, pDir), wl, hl, W, H);
 }
 
 /* Warm-up skip-ahead (photonmap.cl:272-275): `r = rand()*40; for (i=0; i<r; i++) rand();` draws

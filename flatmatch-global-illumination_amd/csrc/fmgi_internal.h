@@ -73,6 +73,7 @@ struct BakeArgs {
     const void *gcells;
     const float *grecs;
     const int32_t *gridx;
+    int grid_axes; /* fJ == {1, 1, 1}: slot a of the image is axis a (ScanGrid's grid_phase1_axes) */
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
     unsigned long long *counts;
     /* AccStream accumulation: deposit codes (texel << 10 | colour state) appended to stream[0..cap) in

@@ -71,9 +71,36 @@ __device__ __forceinline__ float exact_on(cptr<RectDev> R, int i, f3 src, f3 dir
                            dir, closest);
 }
 
-__device__ __forceinline__ float exact_at(const RectDev &r, f3 src, f3 dir, float closest) {
-    return intersect_exact(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz), mkf3(r.wnx, r.wny, r.wnz), r.wl,
-                           mkf3(r.hnx, r.hny, r.hnz), r.hl, src, dir, closest);
+/* The scan's result and what the deposit needs of the hit rect, read once (phase 2 of the fast scans
+   evaluates the winner exactly; the hit stage reuses its in-rect coordinates, see intersect_exact_uv). */
+struct HitRec {
+    int idx;             /* hit rect, or -1 (best = INFINITY: the photon escapes)          */
+    float best, dx, dy;  /* exact hit distance and in-rect coordinates (photonmap.cl:99-100) */
+    float nx, ny, nz, wl, hl;
+    int base, W, H;
+    float bux, buy, buz, bvx, bvy, bvz;
+};
+
+/* photonmap.cl:123-158 (closest = INFINITY) on rect idx, filling h's rect fields and dx, dy */
+__device__ __forceinline__ float exact_hit(const BakeArgs &a, int idx, f3 src, f3 dir, HitRec &h) {
+    const RectDev &r = a.rects[idx];
+    h.idx = idx;
+    h.nx = r.nx; h.ny = r.ny; h.nz = r.nz;
+    h.wl = r.wl; h.hl = r.hl;
+    h.base = r.base; h.W = r.W; h.H = r.H;
+    h.bux = r.bux; h.buy = r.buy; h.buz = r.buz;
+    h.bvx = r.bvx; h.bvy = r.bvy; h.bvz = r.bvz;
+    return intersect_exact_uv(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz), mkf3(r.wnx, r.wny, r.wnz), r.wl,
+                              mkf3(r.hnx, r.hny, r.hnz), r.hl, src, dir, h.dx, h.dy);
+}
+
+/* the result of a literal scan (hit, best) as a HitRec (rare paths: ScanExact, fallbacks) */
+__device__ __forceinline__ void finish_hit(const BakeArgs &a, int hit, float best, f3 src, f3 dir, HitRec &h) {
+    h = HitRec{}; /* every field is (re)written here, so none of the caller's phase-2 values stays live */
+    h.idx = -1;
+    if (hit >= 0 && best != INFINITY)
+        exact_hit(a, hit, src, dir, h); /* the same fac again: closest never changes intersects()' fac */
+    h.best = best;
 }
 
 /* ---- scan policies -------------------------------------------------------------------------- */
@@ -98,17 +125,26 @@ struct StageClock {
 
 struct ScanStats {
     StageClock clk;
+    /* per-lane counts of one launch; the counts bounded by scans fit in 32 bits (a lane traces a few
+       dozen work items of <= 800 scans per launch: the grid is occupancy-sized and chunks are memory-
+       sized), rect tests (up to nrects per scan in the literal scan) do not */
     unsigned long long tests = 0;    /* rectangle tests evaluated (phase-1 records + exact tests)   */
-    unsigned long long rescans = 0;  /* fast scan: scans re-done by the literal exact scan          */
-    unsigned long long ties = 0;     /*   ... because the runner-up was within the separation band */
-    unsigned long long invalid = 0;  /*   ... because the phase-1 winner failed the exact test     */
+    uint32_t rescans = 0;            /* fast scan: scans re-done by the literal exact scan          */
+    uint32_t ties = 0;               /*   ... because the runner-up was within the separation band */
+    uint32_t invalid = 0;            /*   ... because the phase-1 winner failed the exact test     */
 };
 
 /* photonmap.cl:189-206, evaluated literally for every rectangle in index order. */
 struct ScanExact {
     static constexpr bool kLds = false;
-    static __device__ __forceinline__ int scan(const BakeArgs &a, const char *, f3 src, f3 dir, float &best,
-                                               ScanStats &st) {
+    static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
+                                                ScanStats &st) {
+        float best;
+        const int hit = literal(a, lds, src, dir, best, st);
+        finish_hit(a, hit, best, src, dir, h);
+    }
+    static __device__ __forceinline__ int literal(const BakeArgs &a, const char *, f3 src, f3 dir, float &best,
+                                                  ScanStats &st) {
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         float bestd = INFINITY;
         int hit = -1;
@@ -171,8 +207,8 @@ __device__ __forceinline__ void filter_axis(const char *img, int J, f3 s, f3 d, 
 
 struct ScanFast {
     static constexpr bool kLds = true;
-    static __device__ __forceinline__ int scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best,
-                                               ScanStats &st) {
+    static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
+                                                ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         filter_axis<0>(lds, a.fJ[0], src, dir, L1, L2, code1);
@@ -191,8 +227,9 @@ struct ScanFast {
         }
         st.tests += (unsigned long long)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
         if (L1 == INFINITY) { /* V is a subset of the (empty) phase-1 set: the photon escapes */
-            best = INFINITY;
-            return -1;
+            h.best = INFINITY;
+            h.idx = -1;
+            return;
         }
         /* phase 2: exact photonmap.cl intersects() of the winner */
         const int A = code1 >> 16, j = code1 & 0xFFFF;
@@ -204,16 +241,18 @@ struct ScanFast {
             const int off = A == 0 ? 0 : (A == 1 ? 64 * a.fJ[0] : 64 * (a.fJ[0] + a.fJ[1]));
             idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
         }
-        const float f = exact_at(a.rects[idx], src, dir, INFINITY);
+        const float f = exact_hit(a, idx, src, dir, h);
         /* separation: the runner-up's phase-1 value must exceed the exact winner by > 2^-12 relative
            (covers the 2^-20 phase-1 error and the 2^-13 early-out slack); false for f = INF */
         if (!(f < 0) && L2 > f * 1.000244140625f) {
-            best = f;
-            return idx;
+            h.best = f;
+            return;
         }
         st.rescans++;
         if (f < 0) st.invalid++; else st.ties++;
-        return ScanExact::scan(a, lds, src, dir, best, st);
+        float best;
+        const int hit = ScanExact::literal(a, lds, src, dir, best, st);
+        finish_hit(a, hit, best, src, dir, h);
     }
 };
 
@@ -356,6 +395,56 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
     }
 }
 
+/*
+ * Phase 1 of ScanGrid when each axis has exactly one plane per class (the closed boxes): slot a of the
+ * image is axis a, so no slot-to-axis selects. The nearest facing plane is visited first; the two others
+ * only when their fac' is within the 2^-11 band above the current L1 (rare: a hit next to an edge).
+ * Why the visit order cannot change the result: every plane holding a key below L1 (1 + 2^-11) is
+ * visited (a skipped plane's f exceeds the current L1 band, and L1 only decreases), so L1 and the winner
+ * are the minimum over all planes; a skipped key exceeds L1 (1 + 2^-11) > f (1 + 2^-12) for the
+ * winner's exact fac f, so the separation test `L2 > f (1 + 2^-12)` has the same outcome with or
+ * without it (grid_phase1_sorted's argument); equal keys fail that test whatever the order.
+ */
+template <int A>
+__device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *img, f3 s, f3 d, float f, float &L1,
+                                                float &L2, int &code1, unsigned &ntest) {
+    constexpr int U = (A == 0) ? 1 : 0;
+    constexpr int V = (A == 2) ? 1 : 2;
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * A + (comp<A>(d) < 0.0f ? 0 : 64), 16);
+    const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
+    grid_cell_tests(a, ((const GridCell *)a.gcells)[grid_cell(p[0], p[1], p[2], uh, vh)], f, uh, vh, L1, L2, code1,
+                    ntest);
+}
+
+__device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
+                                                 float &L2, int &code1, unsigned &ntest) {
+    const float fx0 = (*(const float *)(img + (d.x < 0.0f ? 0 : 64)) - s.x) * __builtin_amdgcn_rcpf(d.x);
+    const float fy0 = (*(const float *)(img + 128 + (d.y < 0.0f ? 0 : 64)) - s.y) * __builtin_amdgcn_rcpf(d.y);
+    const float fz0 = (*(const float *)(img + 256 + (d.z < 0.0f ? 0 : 64)) - s.z) * __builtin_amdgcn_rcpf(d.z);
+    const float fx = fx0 >= 0.0f ? fx0 : INFINITY, fy = fy0 >= 0.0f ? fy0 : INFINITY; /* behind or NaN */
+    const float fz = fz0 >= 0.0f ? fz0 : INFINITY;
+    /* the nearest plane (axis m at fac' fm), with the per-axis values selected once */
+    const bool my = fy < fx;
+    const float fxy = my ? fy : fx;
+    const bool mz = fz < fxy;
+    const float fm = mz ? fz : fxy;
+    if (!(fm < INFINITY)) return;
+    {
+        const int m = mz ? 2 : (my ? 1 : 0);
+        const float dm = mz ? d.z : (my ? d.y : d.x);
+        const float su = (m == 0) ? s.y : s.x, sv = mz ? s.y : s.z;
+        const float du = (m == 0) ? d.y : d.x, dv = mz ? d.y : d.z;
+        const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * m + (dm < 0.0f ? 0 : 64), 16);
+        const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
+        grid_cell_tests(a, ((const GridCell *)a.gcells)[grid_cell(p[0], p[1], p[2], uh, vh)], fm, uh, vh, L1, L2,
+                        code1, ntest);
+    }
+    const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
+    if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0>(a, img, s, d, fx, L1, L2, code1, ntest);
+    if (m != 1 && fy < INFINITY && fy <= L1 * 1.00048828125f) grid_axes_visit<1>(a, img, s, d, fy, L1, L2, code1, ntest);
+    if (m != 2 && fz < INFINITY && fz <= L1 * 1.00048828125f) grid_axes_visit<2>(a, img, s, d, fz, L1, L2, code1, ntest);
+}
+
 /* calls fn(idx) for the rect index of every record that passes grid_axis's candidate test */
 template <int A, class F>
 __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, int J, f3 s, f3 d, F &&fn) {
@@ -420,12 +509,14 @@ struct ScanGrid {
         return -2; /* more candidates than rounds: caller runs the full literal scan */
     }
 
-    static __device__ __forceinline__ int scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best,
-                                               ScanStats &st) {
+    static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
+                                                ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         unsigned ntest = 0;
-        if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
+        if (a.grid_axes) {
+            grid_phase1_axes(a, lds, src, dir, L1, L2, code1, ntest);
+        } else if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
             grid_phase1_sorted(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
             /* floors and ceilings first: in a layout they bound almost every ray, and the x / y walks
@@ -448,23 +539,25 @@ struct ScanGrid {
         st.tests += (unsigned long long)(ntest + (unsigned)a.ngeneral);
         st.clk.lap(ST_SCAN1);
         if (L1 == INFINITY) {
-            best = INFINITY;
-            return -1;
+            h.best = INFINITY;
+            h.idx = -1;
+            return;
         }
         const int idx = code1; /* rect index of the phase-1 winner */
-        const float f = exact_at(a.rects[idx], src, dir, INFINITY);
+        const float f = exact_hit(a, idx, src, dir, h);
         const bool sep = !(f < 0) && L2 > f * 1.000244140625f; /* ScanFast's separation test */
         st.clk.lap(ST_SCAN2);
         if (sep) {
-            best = f;
-            return idx;
+            h.best = f;
+            return;
         }
         st.rescans++;
         if (f < 0) st.invalid++; else st.ties++;
+        float best;
         int r = ordered_exact(a, lds, src, dir, best);
-        if (r == -2) r = ScanExact::scan(a, lds, src, dir, best, st);
+        if (r == -2) r = ScanExact::literal(a, lds, src, dir, best, st);
+        finish_hit(a, r, best, src, dir, h);
         st.clk.lap(ST_FALLBACK);
-        return r;
     }
 };
 
@@ -605,7 +698,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     bool win = false, start = true, pend = false;
     uint64_t item = 0;
     int nev = 0;
-    unsigned long long n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0;
+    uint32_t n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0; /* see ScanStats */
     ScanStats sst;
     WaveStream ws;
 
@@ -663,22 +756,20 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         sst.clk.lap(ST_SAMPLE);
 
         /* ---- stage 2: scan ---- */
-        float best;
-        const int hit = Scan::scan(a, s_img, pos, dir, best, sst);
+        HitRec h;
+        Scan::scan(a, s_img, pos, dir, h, sst);
         n_scan++;
         sst.clk.lap(ST_SCAN1); /* scans without an inner split (ScanExact / ScanFast) */
         bool dep = false;
         uint32_t code = 0;
-        if (best == INFINITY) { /* photonmap.cl:208-209 */
+        if (h.best == INFINITY) { /* photonmap.cl:208-209 */
             start = true;
             n_esc++;
         } else {
         /* ---- stage 3: hit (photonmap.cl:216-258) ---- */
-        const RectDev &h = a.rects[hit];
-        pos = add3(pos, mul3(dir, best));
+        pos = add3(pos, mul3(dir, h.best));
         const f3 hn = mkf3(h.nx, h.ny, h.nz);
-        const int texel = h.base + tile_at(mkf3(h.px, h.py, h.pz), mkf3(h.wnx, h.wny, h.wnz), h.wl,
-                                           mkf3(h.hnx, h.hny, h.hnz), h.hl, h.W, h.H, pos);
+        const int texel = h.base + tile_uv(h.dx, h.dy, h.wl, h.hl, h.W, h.H); /* == tile_at(rect, pos) */
         const bool last = depth + 1 == FMGI_MAX_DEPTH;
         if ((double)pos.z > 0.0005 || rng_next(rng) > 0.75f) {
             const bool floor = pos.z < 1e-5f;
@@ -708,7 +799,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
             EventDev e;
             e.photon = photon;
             e.depth = depth;
-            e.rect = hit;
+            e.rect = h.idx;
             e.texel = texel;
             e.rgb[0] = col.x;
             e.rgb[1] = col.y;
