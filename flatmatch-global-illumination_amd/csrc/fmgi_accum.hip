@@ -156,7 +156,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
         if (e != hipSuccess) return e;
         lds_set = true;
     }
-    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * sb.groups)), dim3(1024), lds, s, sb.sorted, sb.toff,
+    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * sb.groups)), dim3(sb.block > 0 ? sb.block : 1024), lds, s, sb.sorted, sb.toff,
                        sb.cursor, sb.cap, P, sb.groups, (const uint4 *)sb.colpack, lm, num_texels);
     return hipGetLastError();
 }

@@ -452,10 +452,13 @@ struct fmgi_context {
     unsigned long long *d_counts = nullptr;
     long long *d_colfx = nullptr;
     uint32_t *d_colpack = nullptr; /* the same table as u32 {r, g, b, 0} (STREAM fold) */
-    /* STREAM: deposit-code stream + fold buffers, grown on demand (fmgi_accum.hip) */
-    StreamBufs sb{};
-    uint64_t sb_cap_alloc = 0;
-    uint64_t sb_entries_alloc = 0;
+    /* STREAM: deposit-code stream + fold buffers, grown on demand (fmgi_accum.hip); two sets, so the
+       fold of one chunk (on fold_stream) overlaps the bake of the next */
+    StreamBufs sb[2]{};
+    uint64_t sb_cap_alloc[2] = {0, 0};
+    uint64_t sb_entries_alloc[2] = {0, 0};
+    hipStream_t fold_stream = nullptr;
+    hipEvent_t ev_baked[2] = {nullptr, nullptr}, ev_folded[2] = {nullptr, nullptr};
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -530,10 +533,16 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_src_launch0);
     hipFree(c->d_counts);
     hipFree(c->d_colfx);
-    hipFree(c->sb.stream);
-    hipFree(c->sb.sorted);
-    hipFree(c->sb.cursor);
-    hipFree(c->sb.toff);
+    if (c->fold_stream) hipStreamSynchronize(c->fold_stream);
+    for (int k = 0; k < 2; k++) {
+        hipFree(c->sb[k].stream);
+        hipFree(c->sb[k].sorted);
+        hipFree(c->sb[k].cursor);
+        hipFree(c->sb[k].toff);
+        if (c->ev_baked[k]) hipEventDestroy(c->ev_baked[k]);
+        if (c->ev_folded[k]) hipEventDestroy(c->ev_folded[k]);
+    }
+    if (c->fold_stream) hipStreamDestroy(c->fold_stream);
     hipFree(c->d_colpack);
     hipFree(c->d_counter);
     hipFree(c->d_stats);
@@ -590,38 +599,49 @@ static int configure_accum(fmgi_context *c) {
 
 /* STREAM buffers for a bake of `items` work items on `grid` blocks of `block` lanes: every item makes at
    most 800 deposits and every wave wastes at most one partly filled block. */
-static int ensure_stream(fmgi_context *c, uint64_t items, int grid, int block) {
+static uint64_t stream_cap_for(uint64_t items, int grid, int block) {
     const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
-    const uint64_t cap = items * FMGI_EVENTS_PER_ITEM + (waves + 1) * FMGI_STREAM_BLOCK;
+    return items * FMGI_EVENTS_PER_ITEM + (waves + 1) * FMGI_STREAM_BLOCK;
+}
+
+static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block) {
+    return stream_cap_for(items, grid, block) > c->sb_cap_alloc[k];
+}
+
+static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block) {
+    StreamBufs &sb = c->sb[k];
+    const uint64_t cap = stream_cap_for(items, grid, block);
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
     const uint64_t nslices = (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
     const uint64_t entries = (uint64_t)(P + 1) * nslices;
-    if (cap > c->sb_cap_alloc) {
-        hipFree(c->sb.stream);
-        hipFree(c->sb.sorted);
-        c->sb.stream = c->sb.sorted = nullptr;
-        c->sb_cap_alloc = 0;
-        HIPCHK(hipMalloc(&c->sb.stream, cap * sizeof(uint32_t)));
-        HIPCHK(hipMalloc(&c->sb.sorted, cap * sizeof(uint32_t)));
-        c->sb_cap_alloc = cap;
+    if (cap > c->sb_cap_alloc[k]) {
+        hipFree(sb.stream);
+        hipFree(sb.sorted);
+        sb.stream = sb.sorted = nullptr;
+        c->sb_cap_alloc[k] = 0;
+        HIPCHK(hipMalloc(&sb.stream, cap * sizeof(uint32_t)));
+        HIPCHK(hipMalloc(&sb.sorted, cap * sizeof(uint32_t)));
+        c->sb_cap_alloc[k] = cap;
     }
-    if (entries > c->sb_entries_alloc) {
-        hipFree(c->sb.toff);
-        c->sb.toff = nullptr;
-        c->sb_entries_alloc = 0;
-        HIPCHK(hipMalloc(&c->sb.toff, entries * sizeof(uint16_t)));
-        c->sb_entries_alloc = entries;
+    if (entries > c->sb_entries_alloc[k]) {
+        hipFree(sb.toff);
+        sb.toff = nullptr;
+        c->sb_entries_alloc[k] = 0;
+        HIPCHK(hipMalloc(&sb.toff, entries * sizeof(uint16_t)));
+        c->sb_entries_alloc[k] = entries;
     }
-    if (!c->sb.cursor) HIPCHK(hipMalloc(&c->sb.cursor, 64));
-    c->sb.cap = cap;
-    c->sb.colpack = c->d_colpack;
+    if (!sb.cursor) HIPCHK(hipMalloc(&sb.cursor, 64));
+    sb.cap = cap;
+    sb.colpack = c->d_colpack;
     /* k_tile_runs runs one 112-KiB workgroup per CU at a time and tiles carry uneven code counts:
        ~8 rounds of P x groups workgroups balance the tail (box200, 23 tiles: 28.4 ms fold at 89
        groups vs 31.1 ms at 23 and 34.8 ms at 11; flat from ~33 groups up) */
     {
         const int ncu = std::max(1, c->num_cus);
         const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
-        c->sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (8 * ncu + P - 1) / P);
+        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (8 * ncu + P - 1) / P);
+        const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
+        sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
     }
     return FMGI_OK;
 }
@@ -815,6 +835,8 @@ static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace,
        lanes than work items */
     int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, lds_bytes(c, kernel));
     if (per_cu <= 0) per_cu = 4;
+    if (const char *pe = getenv("FMGI_BAKE_WG_PER_CU")) /* experiments: leave room for concurrent folds */
+        if (atoi(pe) > 0) per_cu = std::min(per_cu, atoi(pe));
     uint64_t lanes_max = (uint64_t)c->num_cus * per_cu * block;
     uint64_t lanes = std::min<uint64_t>(items, lanes_max);
     return (int)std::max<uint64_t>(1, (lanes + block - 1) / block);
@@ -846,13 +868,13 @@ static hipError_t time_end(fmgi_context *c, hipStream_t s, hipEvent_t t0, hipEve
     return e;
 }
 
-/* work items per STREAM chunk: codes for 800 deposits per item, twice (stream + sorted), in at most half
-   of the device memory that is free or already held by the stream buffers */
-static uint64_t stream_chunk_items(fmgi_context *c) {
+/* work items per STREAM chunk: codes for 800 deposits per item, twice (stream + sorted), for each of the
+   `sets` buffer sets in use, in at most half of the device memory that is free or already held by them */
+static uint64_t stream_chunk_items(fmgi_context *c, int sets) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
-    const double avail = (double)fr + 8.0 * (double)c->sb_cap_alloc;
-    uint64_t items = (uint64_t)(avail * 0.5 / (2.0 * 4.0 * FMGI_EVENTS_PER_ITEM));
+    const double avail = (double)fr + 8.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]);
+    uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * 2.0 * 4.0 * FMGI_EVENTS_PER_ITEM));
     /* slices are indexed in 32 bits by the sort kernel's grid */
     const uint64_t max_items = ((1ull << 31) - 1) / FMGI_EVENTS_PER_ITEM * FMGI_STREAM_SLICE;
     items = std::min(items, max_items);
@@ -925,27 +947,65 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         return FMGI_OK;
     }
     /* STREAM: the codes of a chunk of work items are held in HBM (2 x 4 B per deposit, worst case 800
-       deposits per item); the chunk is sized from the free device memory (at most half of it) */
-    const uint64_t chunk = stream_chunk_items(c);
-    for (uint64_t cb = b; cb < e; cb += chunk) {
+       deposits per item); chunks are memory-sized and fold after their bake on s.
+       FMGI_PIPELINE=P > 1 (experiment) cuts the items into >= P chunks (every lane still tracing >= 4
+       items per chunk) and folds chunk k on the context's fold stream while chunk k + 1 bakes into the
+       other buffer set. Measured on box200 (profiles/r01/s36, s37): slower for every P, fold block size
+       and bake occupancy tried, because the persistent bake leaves the folds no room to run beside it,
+       so the default is 1. */
+    const uint64_t n = e - b;
+    const int lanes = grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block;
+    int pipeline = 1;
+    if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
+    uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1);
+    if (pipeline > 1) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>((n + pipeline - 1) / pipeline, 4 * (uint64_t)lanes));
+    chunk = std::max<uint64_t>(chunk, 1);
+    const bool overlap = pipeline > 1 && chunk < n;
+    if (overlap) {
+        if (!c->fold_stream) HIPCHK(hipStreamCreateWithFlags(&c->fold_stream, hipStreamNonBlocking));
+        for (int k = 0; k < 2; k++) {
+            if (!c->ev_baked[k]) HIPCHK(hipEventCreateWithFlags(&c->ev_baked[k], hipEventDisableTiming));
+            if (!c->ev_folded[k]) HIPCHK(hipEventCreateWithFlags(&c->ev_folded[k], hipEventDisableTiming));
+        }
+    }
+    hipStream_t fs = overlap ? c->fold_stream : s;
+    int nchunk = 0;
+    for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
+        const int k = nchunk & 1;
         const int grid = grid_blocks(c, kernel, c->accum, trace, block, ce - cb);
-        int rc = ensure_stream(c, ce - cb, grid, block);
+        /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
+           happens only while growing, after a full wait) */
+        if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));
+        if (ensure_stream_needs_growth(c, k, ce - cb, grid, block)) { /* no fold may still read it */
+            HIPCHK(hipStreamSynchronize(s));
+            if (c->fold_stream) HIPCHK(hipStreamSynchronize(c->fold_stream));
+        }
+        int rc = ensure_stream(c, k, ce - cb, grid, block);
         if (rc != FMGI_OK) return rc;
+        StreamBufs &sb = c->sb[k];
         a.item_begin = cb;
         a.item_end = ce;
-        a.stream = c->sb.stream;
-        a.stream_cap = c->sb.cap;
-        a.stream_cursor = c->sb.cursor;
+        a.stream = sb.stream;
+        a.stream_cap = sb.cap;
+        a.stream_cursor = sb.cursor;
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
-        HIPCHK(hipMemsetAsync(c->sb.cursor, 0, 8, s));
+        HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
         HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid, block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
-        HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_stream_fold(c->sb, c->num_texels, (unsigned long long *)lm, s));
-        HIPCHK(time_end(c, s, t0, t1, c->ev_fold));
+        if (overlap) {
+            HIPCHK(hipEventRecord(c->ev_baked[k], s));
+            HIPCHK(hipStreamWaitEvent(fs, c->ev_baked[k], 0));
+        }
+        HIPCHK(time_begin(c, fs, t0));
+        HIPCHK(fmgi_stream_fold(sb, c->num_texels, (unsigned long long *)lm, fs));
+        HIPCHK(time_end(c, fs, t0, t1, c->ev_fold));
+        if (overlap) HIPCHK(hipEventRecord(c->ev_folded[k], fs));
+    }
+    if (overlap) { /* everything after this call on s sees the complete lightmap */
+        HIPCHK(hipStreamWaitEvent(s, c->ev_folded[(nchunk - 1) & 1], 0));
     }
     return FMGI_OK;
 }
@@ -1105,6 +1165,25 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
     if (err == hipSuccess) err = hipMemcpy(co, d + 2 * n, (size_t)n * 4, hipMemcpyDeviceToHost);
     hipFree(d);
     if (err != hipSuccess) return set_err(FMGI_ERR_HIP, "device sincos: %s", hipGetErrorString(err));
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_device_unit(fmgi_context *c, int op, const float *a, const float *b, int32_t *out, int64_t n) {
+    if (!c || n < 0 || !a || !out || (op == FMGI_UNIT_TRUNC_DIV && !b) ||
+        (op != FMGI_UNIT_SQRT && op != FMGI_UNIT_TRUNC_DIV))
+        return set_err(FMGI_ERR_ARG, "bad arguments");
+    if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
+    if (!n) return FMGI_OK;
+    HIPCHK(hipSetDevice(c->device));
+    float *d = nullptr;
+    HIPCHK(hipMalloc(&d, (size_t)n * 12));
+    hipError_t err = hipMemcpy(d, a, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (err == hipSuccess && b) err = hipMemcpy(d + n, b, (size_t)n * 4, hipMemcpyHostToDevice);
+    if (err == hipSuccess) err = fmgi_launch_unit(op, d, d + n, (int32_t *)(d + 2 * n), n, c->stream);
+    if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
+    if (err == hipSuccess) err = hipMemcpy(out, d + 2 * n, (size_t)n * 4, hipMemcpyDeviceToHost);
+    hipFree(d);
+    if (err != hipSuccess) return set_err(FMGI_ERR_HIP, "device unit: %s", hipGetErrorString(err));
     return FMGI_OK;
 }
 

@@ -91,15 +91,31 @@ FMGI_HD void sampler_basis(f3 n, f3 &bu, f3 &bv) {
     bv = vdir;
 }
 
+/* Correctly rounded sqrtf (== sqrtf bit for bit) for x == 0 and 2^-96 <= x < inf: v_sqrt_f32 plus one
+   residual correction, i.e. LLVM's gfx9 expansion without its rescaling of tiny inputs. The samplers'
+   arguments are rand() in {0} u [2^-32, 1] and 1 - r*r in {0} u [2^-24, 1]. */
+FMGI_HD float sqrt_cr(float x) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float y = __builtin_amdgcn_sqrtf(x);
+    const float ym = __int_as_float(__float_as_int(y) - 1), yp = __int_as_float(__float_as_int(y) + 1);
+    const float rm = fmaf(-ym, y, x), rp = fmaf(-yp, y, x);
+    float q = rm <= 0.0f ? ym : y;
+    q = rp > 0.0f ? yp : q;
+    return x == 0.0f ? x : q;
+#else
+    return sqrtf(x);
+#endif
+}
+
 /* photonmap.cl:27-74 with the basis precomputed: fold=1 is the window ("sky") sampler. */
 FMGI_HD f3 sample_dir(uint32_t &rng, f3 n, f3 bu, f3 bv, bool fold) {
-    float r = sqrtf(rng_next(rng));
+    float r = sqrt_cr(rng_next(rng));
     float phi = 6.283184f * rng_next(rng);
     float sn, cs;
     fmgi_sincosf(phi, &sn, &cs);
     float u = r * cs;
     float v = r * sn;
-    float w = sqrtf(1.0f - r * r);
+    float w = sqrt_cr(1.0f - r * r);
     if (fold && u < 0) u = -u;
     return add3(add3(mul3(bu, u), mul3(bv, v)), mul3(n, w));
 }
@@ -137,10 +153,23 @@ FMGI_HD float intersect_exact_uv(f3 n, f3 pos, f3 wn, float wl, f3 hn, float hl,
     return fac;
 }
 
+/* (int)(x / y) for 0 <= x / y < 2^30 (correctly rounded quotient, truncated). On the device: the
+   quotient through v_rcp_f32 is within 2^-21 relative of x / y and of its rounding, so when both ends of
+   the +-2^-20 band around it truncate to the same integer, that integer is the answer; otherwise (a
+   quotient next to an integer) the exact division decides. */
+FMGI_HD int trunc_div(float x, float y) {
+#if defined(__HIP_DEVICE_COMPILE__)
+    const float q = x * __builtin_amdgcn_rcpf(y);
+    const int lo = (int)(q * 0.99999904632568359375f), hi = (int)(q * 1.00000095367431640625f);
+    if (lo == hi) return lo;
+#endif
+    return (int)(x / y);
+}
+
 /* photonmap.cl:108-119: the tile of in-rect coordinates (dx, dy) */
 FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, int W, int H) {
-    int tx = (int)(dx * (float)W / wl);
-    int ty = (int)(dy * (float)H / hl);
+    int tx = trunc_div(dx * (float)W, wl);
+    int ty = trunc_div(dy * (float)H, hl);
     tx = tx < 0 ? 0 : (tx > W - 1 ? W - 1 : tx);
     ty = ty < 0 ? 0 : (ty > H - 1 ? H - 1 : ty);
     return ty * W + tx;

@@ -106,6 +106,7 @@ struct StreamBufs {
     uint16_t *toff;             /* per slice: P + 1 run offsets (the last = valid codes)        */
     const uint32_t *colpack;    /* colour table as u32 {r, g, b, 0} per state (fixed point)      */
     int groups;                 /* slice groups per tile in the sum kernel                      */
+    int block;                  /* threads per sum workgroup (256, 512 or 1024)                  */
 };
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);
 
@@ -121,5 +122,6 @@ hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long
 hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, float *tout, int64_t n,
                                 hipStream_t s);
 hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, hipStream_t s);
+hipError_t fmgi_launch_unit(int op, const float *a, const float *b, int32_t *out, int64_t n, hipStream_t s);
 
 #endif

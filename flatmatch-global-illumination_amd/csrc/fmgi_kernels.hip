@@ -771,7 +771,12 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         const f3 hn = mkf3(h.nx, h.ny, h.nz);
         const int texel = h.base + tile_uv(h.dx, h.dy, h.wl, h.hl, h.W, h.H); /* == tile_at(rect, pos) */
         const bool last = depth + 1 == FMGI_MAX_DEPTH;
-        if ((double)pos.z > 0.0005 || rng_next(rng) > 0.75f) {
+        /* the basis of a diffuse sample at the top of the next iteration (unused unless pend is set) */
+        sn = hn;
+        sbu = mkf3(h.bux, h.buy, h.buz);
+        sbv = mkf3(h.bvx, h.bvy, h.bvz);
+        /* (double)pos.z > 0.0005 (photonmap.cl:236) <=> pos.z > the largest float below 0.0005 */
+        if (pos.z > 4.99999965541064739227294921875e-4f || rng_next(rng) > 0.75f) {
             const bool floor = pos.z < 1e-5f;
             if (floor) {
                 col.y *= 0.85f;
@@ -783,9 +788,6 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 rng = lcg2(rng); /* the direction of a photon that ends here is never used */
             } else {
                 pend = true; /* sampled at the top of the next iteration */
-                sn = hn;
-                sbu = mkf3(h.bux, h.buy, h.buz);
-                sbv = mkf3(h.bvx, h.bvy, h.bvz);
             }
         } else {
             const float two = 2.0f * dot3(hn, dir);
@@ -887,6 +889,14 @@ __global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, flo
     c[i] = b;
 }
 
+/* the bake's arithmetic helpers, one element per thread (fmgi_device_unit) */
+__global__ void k_unit(int op, const float *__restrict__ a, const float *__restrict__ b, int32_t *__restrict__ out,
+                       int64_t n) {
+    int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    out[i] = op == 0 ? __float_as_int(sqrt_cr(a[i])) : trunc_div(a[i], b[i]);
+}
+
 template <class Scan, class Acc>
 void launch3(const BakeArgs &a, bool trace, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
     if (trace)
@@ -970,6 +980,12 @@ hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, 
 hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long *src, int64_t n, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_add_u64, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, dst, src, n);
+    return hipGetLastError();
+}
+
+hipError_t fmgi_launch_unit(int op, const float *a, const float *b, int32_t *out, int64_t n, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_unit, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, op, a, b, out, n);
     return hipGetLastError();
 }
 

@@ -52,15 +52,12 @@ FMGI_HD void fmgi_sincosf(float xf, float *sf, float *cf) {
     double r = (x - dk * P1) - dk * P2;
     double s, c;
     fmgi_sincos_kernel(r, &s, &c);
-    double so, co;
-    switch (k & 3) {
-    case 0: so = s; co = c; break;
-    case 1: so = c; co = -s; break;
-    case 2: so = -s; co = -c; break;
-    default: so = -c; co = s; break;
-    }
-    *sf = (float)so;
-    *cf = (float)co;
+    /* quadrant k: (sin, cos) = (s, c), (c, -s), (-s, -c), (-c, s); rounding to float commutes with
+       negation, so the swap and the signs are applied after it (selects, no branches) */
+    const float s32 = (float)s, c32 = (float)c;
+    const float so = (k & 1) ? c32 : s32, co = (k & 1) ? s32 : c32;
+    *sf = (k & 2) ? -so : so;
+    *cf = ((k + 1) & 2) ? -co : co;
 }
 
 #endif

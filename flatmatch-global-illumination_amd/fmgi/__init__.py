@@ -55,6 +55,10 @@ __all__ = [
 ]
 
 
+UNIT_SQRT = 0       # fmgi_device_unit ops (include/flatmatch_gi.h)
+UNIT_TRUNC_DIV = 1
+
+
 def _ptr(a: np.ndarray | None):
     if a is None or len(a) == 0:
         return None
@@ -205,6 +209,16 @@ class Context:
         c = np.empty_like(x)
         check(self.lib.fmgi_device_sincosf(self.h, _ptr(x), _ptr(s), _ptr(c), len(x)), "fmgi_device_sincosf")
         return s, c
+
+    def device_unit(self, op: int, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:
+        """The bake's device arithmetic helpers (include/flatmatch_gi.h fmgi_device_unit): op 0 = the
+        sampler's sqrtf (returns float32), op 1 = (int)(a / b) of the tile index (returns int32)."""
+        a = np.ascontiguousarray(a, np.float32)
+        bb = None if b is None else np.ascontiguousarray(b, np.float32)
+        out = np.empty(len(a), np.int32)
+        check(self.lib.fmgi_device_unit(self.h, op, _ptr(a), None if bb is None else _ptr(bb), _ptr(out), len(a)),
+              "fmgi_device_unit")
+        return out.view(np.float32) if op == 0 else out
 
 
 GRID_PLANE_DTYPE = np.dtype([("plane", "<f4"), ("u0", "<f4"), ("v0", "<f4"), ("iu", "<f4"), ("iv", "<f4"),

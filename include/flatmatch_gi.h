@@ -261,6 +261,12 @@ int fmgi_grid_copy(const fmgi_context *ctx, void *planes, void *cells, float *re
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);
 /* Device-side twin of fmgi_host_sincosf over n inputs (synchronous; for parity tests). */
 int fmgi_device_sincosf(fmgi_context *ctx, const float *x, float *s, float *c, int64_t n);
+/* Device arithmetic helpers of the bake kernel over n inputs (synchronous; for parity tests):
+   op FMGI_UNIT_SQRT: out[i] = bits of the sampler's correctly rounded sqrtf(a[i]) (b unused);
+   op FMGI_UNIT_TRUNC_DIV: out[i] = (int)(a[i] / b[i]), the tile index step of photonmap.cl:108-109. */
+#define FMGI_UNIT_SQRT 0
+#define FMGI_UNIT_TRUNC_DIV 1
+int fmgi_device_unit(fmgi_context *ctx, int op, const float *a, const float *b, int32_t *out, int64_t n);
 
 #ifdef __cplusplus
 }

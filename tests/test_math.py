@@ -31,3 +31,13 @@ def test_library_sincos_matches_numpy_double_rounding():
     s, c = fmgi.host_sincosf(xs)
     assert np.array_equal(s, np.sin(xs.astype(np.float64)).astype(np.float32))
     assert np.array_equal(c, np.cos(xs.astype(np.float64)).astype(np.float32))
+
+
+def test_roulette_threshold_is_the_double_comparison():
+    """k_bake tests photonmap.cl:236's `(double)pos.z > 0.0005` as `pos.z > c` with c the largest float
+    below 0.0005: the two agree on every float (checked on the floats around the threshold and signs)."""
+    c = np.float32(4.99999965541064739227294921875e-4)
+    assert float(c) < 0.0005 < float(np.nextafter(c, np.float32(1)))
+    z = c.view(np.uint32) + np.arange(-4096, 4097, dtype=np.int64)
+    zf = np.concatenate([z.astype(np.uint32).view(np.float32), [0.0, -0.0, -c, 1.0, 1e-5, np.inf]]).astype(np.float32)
+    assert np.array_equal(zf.astype(np.float64) > 0.0005, zf > c)
