@@ -125,13 +125,12 @@ struct StageClock {
 
 struct ScanStats {
     StageClock clk;
-    /* per-lane counts of one launch; the counts bounded by scans fit in 32 bits (a lane traces a few
-       dozen work items of <= 800 scans per launch: the grid is occupancy-sized and chunks are memory-
-       sized), rect tests (up to nrects per scan in the literal scan) do not */
-    unsigned long long tests = 0;    /* rectangle tests evaluated (phase-1 records + exact tests)   */
-    uint32_t rescans = 0;            /* fast scan: scans re-done by the literal exact scan          */
-    uint32_t ties = 0;               /*   ... because the runner-up was within the separation band */
-    uint32_t invalid = 0;            /*   ... because the phase-1 winner failed the exact test     */
+    /* rectangle tests evaluated (phase-1 records + exact tests) since the lane's last work-item fetch,
+       where they are flushed (flush_tests): a work item makes <= 800 scans of <= nrects tests each */
+    uint32_t tests = 0;
+    /* scans re-done by the literal scan (rescans = ties + invalid; <= the lane's scans, 32 bits) */
+    uint32_t ties = 0;    /* the runner-up was within the separation band */
+    uint32_t invalid = 0; /* the phase-1 winner failed the exact test     */
 };
 
 /* photonmap.cl:189-206, evaluated literally for every rectangle in index order. */
@@ -153,7 +152,7 @@ struct ScanExact {
             if (d < 0) continue;
             if (d < bestd) { bestd = d; hit = i; }
         }
-        st.tests += (unsigned long long)a.nrects;
+        st.tests += (uint32_t)a.nrects;
         best = bestd;
         return hit;
     }
@@ -225,7 +224,7 @@ struct ScanFast {
             code1 = lt ? ((3 << 16) | g) : code1;
             L1 = lt ? key : L1;
         }
-        st.tests += (unsigned long long)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
+        st.tests += (uint32_t)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
         if (L1 == INFINITY) { /* V is a subset of the (empty) phase-1 set: the photon escapes */
             h.best = INFINITY;
             h.idx = -1;
@@ -248,7 +247,6 @@ struct ScanFast {
             h.best = f;
             return;
         }
-        st.rescans++;
         if (f < 0) st.invalid++; else st.ties++;
         float best;
         const int hit = ScanExact::literal(a, lds, src, dir, best, st);
@@ -536,7 +534,7 @@ struct ScanGrid {
             code1 = lt ? G[g] : code1;
             L1 = lt ? key : L1;
         }
-        st.tests += (unsigned long long)(ntest + (unsigned)a.ngeneral);
+        st.tests += ntest + (uint32_t)a.ngeneral;
         st.clk.lap(ST_SCAN1);
         if (L1 == INFINITY) {
             h.best = INFINITY;
@@ -551,7 +549,6 @@ struct ScanGrid {
             h.best = f;
             return;
         }
-        st.rescans++;
         if (f < 0) st.invalid++; else st.ties++;
         float best;
         int r = ordered_exact(a, lds, src, dir, best);
@@ -698,7 +695,9 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     bool win = false, start = true, pend = false;
     uint64_t item = 0;
     int nev = 0;
-    uint32_t n_ph = 0, n_scan = 0, n_dep = 0, n_esc = 0; /* see ScanStats */
+    /* per-lane counts of one launch, in 32 bits: a lane traces a few dozen work items per launch (the
+       grid is occupancy-sized, chunks are memory-sized); scans = deposits + escapes */
+    uint32_t n_ph = 0, n_dep = 0, n_esc = 0;
     ScanStats sst;
     WaveStream ws;
 
@@ -711,6 +710,10 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 if (TRACE && photon >= 0) {
                     a.ev_counts[item - a.item_begin] = nev;
                     a.rng_final[item - a.item_begin] = rng;
+                }
+                if (sst.tests) { /* flush this lane's rect-test count (see ScanStats) */
+                    atomicAdd(a.stats + KSTAT_TESTS, (unsigned long long)sst.tests);
+                    sst.tests = 0;
                 }
                 const uint64_t w = a.item_begin + atomicAdd(a.counter, 1ull);
                 if (w >= a.item_end) break;
@@ -758,7 +761,6 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         /* ---- stage 2: scan ---- */
         HitRec h;
         Scan::scan(a, s_img, pos, dir, h, sst);
-        n_scan++;
         sst.clk.lap(ST_SCAN1); /* scans without an inner split (ScanExact / ScanFast) */
         bool dep = false;
         uint32_t code = 0;
@@ -823,11 +825,14 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         a.rng_final[item - a.item_begin] = rng;
     }
 
-    unsigned long long v[KSTAT_N] = {n_ph, n_scan, n_dep, n_esc, sst.rescans, sst.tests, sst.ties, sst.invalid};
+    const unsigned long long v[8] = {n_ph, (unsigned long long)n_dep + n_esc, n_dep, n_esc, sst.tests,
+                                     (unsigned long long)sst.ties + sst.invalid, sst.ties, sst.invalid};
+    const int slot[8] = {KSTAT_PHOTONS, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_TESTS, KSTAT_RESCANS,
+                         KSTAT_TIES, KSTAT_INVALID};
 #pragma unroll
-    for (int i = 0; i < KSTAT_N; i++) {
+    for (int i = 0; i < 8; i++) {
         unsigned long long s = wave_sum(v[i]);
-        if ((threadIdx.x & 63) == 0 && s) atomicAdd(a.stats + i, s);
+        if ((threadIdx.x & 63) == 0 && s) atomicAdd(a.stats + slot[i], s);
     }
 #ifdef FMGI_STAGE_TIMING
     if ((threadIdx.x & 63) == 0)
