@@ -11,8 +11,9 @@
  *   sort : per 8192-code slice, a counting sort by 4096-texel tile in LDS, written back contiguously,
  *          plus the slice's tile offsets (u16)                                         k_slice_sort
  *   sum  : one workgroup per (tile, group of slices) reads that tile's run of every slice of its group
- *          and sums it exactly in LDS (int64 RGB per texel, ds_add_u64), then adds the tile to the
- *          lightmap with one coalesced atomic per texel channel                         k_tile_runs
+ *          and sums it exactly in LDS (int64 R, G - R, B - R per texel, ds_add_u64: a grey deposit
+ *          is one add), then adds the tile to the lightmap with one coalesced atomic per channel
+ *                                                                                      k_tile_runs
  *
  * HBM traffic per deposit: 4 B written by the bake, 4 B read + 4 B written by the sort, 4 B read by the
  * sum. Every step is exact integer arithmetic, so the lightmap is bit-identical to the atomic paths.
@@ -98,15 +99,17 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
                                                    const unsigned long long *__restrict__ n_ptr, uint64_t cap,
                                                    int P, int G, const uint4 *__restrict__ colpack,
                                                    unsigned long long *__restrict__ lm, int num_texels) {
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* [4096][3] + colours */
-    unsigned long long *acc = s_acc;
+    /* per texel of the tile: sum R, sum (G - R), sum (B - R) (int64 modulo 2^64; the true sums of G and
+       B are non-negative), so a grey code costs one LDS add and a tinted one three */
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [4096] + colours */
+    unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
     const int t = blockIdx.x / G, g = blockIdx.x % G;
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
     const uint64_t ns = (n + kSlice - 1) / kSlice;
     const uint64_t b_lo = ns * g / G, b_hi = ns * (g + 1) / G;
     if (b_lo >= b_hi) return; /* uniform */
-    for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) acc[i] = 0;
+    for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
     for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
@@ -127,17 +130,21 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
                 if (v[u] == kSentinel) continue;
                 const int tx = (int)((v[u] >> 10) & (kTileTexels - 1));
                 const uint4 cc = col[v[u] & 1023];
-                atomicAdd(&acc[3 * tx + 0], (unsigned long long)cc.x);
-                atomicAdd(&acc[3 * tx + 1], (unsigned long long)cc.y);
-                atomicAdd(&acc[3 * tx + 2], (unsigned long long)cc.z);
+                atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
+                if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
+                if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
             }
         }
     }
     __syncthreads();
-    for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) {
-        const unsigned long long v = acc[i];
-        const int texel = t * kTileTexels + i / 3;
-        if (v && texel < num_texels) atomicAdd(lm + 4 * (size_t)texel + (i % 3), v);
+    for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
+        const int texel = t * kTileTexels + i;
+        if (texel >= num_texels) break;
+        const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
+        unsigned long long *q = lm + 4 * (size_t)texel;
+        if (r) atomicAdd(q + 0, r);
+        if (gg) atomicAdd(q + 1, gg);
+        if (bb) atomicAdd(q + 2, bb);
     }
 }
 

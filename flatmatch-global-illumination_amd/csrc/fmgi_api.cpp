@@ -558,13 +558,19 @@ static const int kStreamMaxTexels = FMGI_MAX_TILES << FMGI_TILE_BITS; /* 4,194,3
 static int ensure_colour_table(fmgi_context *c) {
     if (c->d_colfx) return FMGI_OK;
     std::vector<long long> t = colour_table();
+    /* the STREAM fold's table: {R, G - R, B - R} per state (differences as two's complement 32-bit), so
+       a grey deposit (R = G = B: a window's photon before any floor bounce) is one LDS add */
     std::vector<uint32_t> p((size_t)FMGI_COLOUR_STATES * 4, 0u);
-    for (int sid = 0; sid < FMGI_COLOUR_STATES; sid++)
+    for (int sid = 0; sid < FMGI_COLOUR_STATES; sid++) {
         for (int k = 0; k < 3; k++) {
-            const long long v = t[3 * sid + k]; /* <= 18 * 2^25 < 2^32 */
-            if (v < 0 || v > (long long)UINT32_MAX) return set_err(FMGI_ERR_STATE, "colour table overflow");
-            p[4 * sid + k] = (uint32_t)v;
+            const long long v = t[3 * sid + k]; /* <= 18 * 2^25 < 2^30 */
+            if (v < 0 || v >= (1ll << 30)) return set_err(FMGI_ERR_STATE, "colour table overflow");
         }
+        const long long r = t[3 * sid];
+        p[4 * sid + 0] = (uint32_t)r;
+        p[4 * sid + 1] = (uint32_t)(int32_t)(t[3 * sid + 1] - r);
+        p[4 * sid + 2] = (uint32_t)(int32_t)(t[3 * sid + 2] - r);
+    }
     HIPCHK(hipMalloc(&c->d_colfx, t.size() * sizeof(long long)));
     HIPCHK(hipMemcpy(c->d_colfx, t.data(), t.size() * sizeof(long long), hipMemcpyHostToDevice));
     HIPCHK(hipMalloc(&c->d_colpack, p.size() * sizeof(uint32_t)));

@@ -104,7 +104,8 @@ struct StreamBufs {
     unsigned long long *cursor; /* reserved codes (device)                                      */
     uint32_t *sorted;           /* per 8192-code slice: its codes sorted by tile, cap entries    */
     uint16_t *toff;             /* per slice: P + 1 run offsets (the last = valid codes)        */
-    const uint32_t *colpack;    /* colour table as u32 {r, g, b, 0} per state (fixed point)      */
+    const uint32_t *colpack;    /* colour table {R, G - R, B - R, 0} per state (fixed point, the
+                                   differences two's complement)                                */
     int groups;                 /* slice groups per tile in the sum kernel                      */
     int block;                  /* threads per sum workgroup (256, 512 or 1024)                  */
 };
