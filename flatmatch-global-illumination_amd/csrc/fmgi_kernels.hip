@@ -764,6 +764,11 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         sst.clk.lap(ST_SCAN1); /* scans without an inner split (ScanExact / ScanFast) */
         bool dep = false;
         uint32_t code = 0;
+        /* the basis of a diffuse sample at the top of the next iteration (unused unless pend is set; an
+           escaped photon's next sample is an emission, whose basis the start block sets) */
+        sn = mkf3(h.nx, h.ny, h.nz);
+        sbu = mkf3(h.bux, h.buy, h.buz);
+        sbv = mkf3(h.bvx, h.bvy, h.bvz);
         if (h.best == INFINITY) { /* photonmap.cl:208-209 */
             start = true;
             n_esc++;
@@ -773,10 +778,6 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         const f3 hn = mkf3(h.nx, h.ny, h.nz);
         const int texel = h.base + tile_uv(h.dx, h.dy, h.wl, h.hl, h.W, h.H); /* == tile_at(rect, pos) */
         const bool last = depth + 1 == FMGI_MAX_DEPTH;
-        /* the basis of a diffuse sample at the top of the next iteration (unused unless pend is set) */
-        sn = hn;
-        sbu = mkf3(h.bux, h.buy, h.buz);
-        sbv = mkf3(h.bvx, h.bvy, h.bvz);
         /* (double)pos.z > 0.0005 (photonmap.cl:236) <=> pos.z > the largest float below 0.0005 */
         if (pos.z > 4.99999965541064739227294921875e-4f || rng_next(rng) > 0.75f) {
             const bool floor = pos.z < 1e-5f;
