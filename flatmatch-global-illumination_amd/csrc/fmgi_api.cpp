@@ -964,6 +964,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
     uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1);
+    if (const char *ce = getenv("FMGI_CHUNK_ITEMS")) /* tests: force several chunks */
+        if (atoll(ce) > 0) chunk = std::min<uint64_t>(chunk, (uint64_t)atoll(ce));
     if (pipeline > 1) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>((n + pipeline - 1) / pipeline, 4 * (uint64_t)lanes));
     chunk = std::max<uint64_t>(chunk, 1);
     const bool overlap = pipeline > 1 && chunk < n;
@@ -978,7 +980,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     int nchunk = 0;
     for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
-        const int k = nchunk & 1;
+        const int k = overlap ? (nchunk & 1) : 0; /* one buffer set unless the folds run beside the bakes */
         const int grid = grid_blocks(c, kernel, c->accum, trace, block, ce - cb);
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */

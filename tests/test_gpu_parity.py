@@ -151,12 +151,22 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     ctx.set_accumulation(fmgi.ACCUM_FX3)
     c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
     ctx.set_accumulation(fmgi.ACCUM_STREAM)
-    d = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)  # 3 chunks of <= 4e6 items
+    d = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)  # one memory-sized chunk
+    os.environ["FMGI_CHUNK_ITEMS"] = "3000000"  # four chunks through one buffer set ...
+    try:
+        e = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+        os.environ["FMGI_PIPELINE"] = "3"  # ... and with each fold beside the next chunk's bake
+        f = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+    finally:
+        os.environ.pop("FMGI_CHUNK_ITEMS", None)
+        os.environ.pop("FMGI_PIPELINE", None)
     d1 = _bake_gpu(torch_cuda, ctx, 0, 12_345, fmgi.KERNEL_GRID)
     d2 = _bake_gpu(torch_cuda, ctx, 12_345, n, fmgi.KERNEL_GRID)
     assert np.array_equal(a, b1 + b2)
     assert np.array_equal(a, c)  # the accumulation modes agree bit for bit
     assert np.array_equal(a, d)
+    assert np.array_equal(a, e)
+    assert np.array_equal(a, f)
     assert np.array_equal(a, d1 + d2)
     assert ctx.stats()["stream_overflow"] == 0
     ctx.reset_stats()
