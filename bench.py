@@ -40,6 +40,8 @@ CONFIGS = {
 METRIC = "photons/sec + achieved HBM GB/s (% of peak), 200-rect scene, 1/2/4/8 MI355X"
 FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector == FP32 matrix peak on gfx950
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles at 2.4 GHz
+VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
 
 
 def load_scene(name):
@@ -86,6 +88,18 @@ def pmc_traffic(config_name):
     except (OSError, ValueError):
         return None
     return d.get("hbm_bytes_per_launch") if "k_bake" in d.get("kernel", "") else None
+
+
+def sq_valu(config_name):
+    """SQ_INSTS_VALU per bake launch from the committed rocprofv3 SQ summary (profiles/), if present."""
+    p = os.path.join(REPO, "profiles", "sq_issue.json")
+    if not os.path.exists(p):
+        return None
+    try:
+        d = json.load(open(p)).get(config_name, {})
+    except (OSError, ValueError):
+        return None
+    return d.get("per_launch", {}).get("SQ_INSTS_VALU")
 
 
 def main():
@@ -268,12 +282,19 @@ def main():
                 "algorithmic_bytes_per_launch": hbm_bytes,
                 "binding": binding,
                 "atomics": atomics,
+                # the binding resource: VALU instruction issue (wave-instructions per launch from the committed
+                # SQ_INSTS_VALU profile of this config, over the live HIP-event kernel time)
+                "issue": (None if sq_valu(args.config) is None else {
+                    "achieved": sq_valu(args.config) / ks, "peak": VALU_PEAK_INSTS, "unit": "wave-VALU-instr/s",
+                    "frac": sq_valu(args.config) / ks / VALU_PEAK_INSTS,
+                    "valu_insts_per_launch": sq_valu(args.config),
+                    "source": "profiles/sq_issue.json (rocprofv3 --pmc SQ_INSTS_VALU)"}),
                 "compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
                             "frac": achieved_tf / FP32_PEAK_TFLOPS,
                             "algorithmic_flops_per_launch": flops,
-                            "note": "SURVEY.md §8d brute-force accounting (40 flops/rect test + 150/scan); the fast "
-                                    "scan does ~15 VALU ops per front-facing test, so frac > 1 measures the "
-                                    "algorithmic saving, not the hardware"},
+                            "note": "SURVEY.md §8d brute-force accounting (40 flops/rect test + 150/scan) of the "
+                                    "linear scan the grid replaces, so frac > 1 measures the algorithmic saving, "
+                                    "not the hardware; the hardware figure is `issue`"},
             },
             "per_photon": {
                 "scans": scans / photons_done,

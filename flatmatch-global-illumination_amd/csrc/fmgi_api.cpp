@@ -75,6 +75,8 @@ RectDev make_rect(const fmgi_rect &r) {
     f3 wn = div3(w, wl), hn = div3(h, hl);
     d.wnx = wn.x; d.wny = wn.y; d.wnz = wn.z; d.wl = wl;
     d.hnx = hn.x; d.hny = hn.y; d.hnz = hn.z; d.hl = hl;
+    d.iwl = 1.0f / wl;
+    d.ihl = 1.0f / hl;
     d.base = r.lightmapSetup[0];
     d.W = r.lightmapSetup[1];
     d.H = r.lightmapSetup[2];
@@ -1177,8 +1179,8 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
 }
 
 FMGI_API int fmgi_device_unit(fmgi_context *c, int op, const float *a, const float *b, int32_t *out, int64_t n) {
-    if (!c || n < 0 || !a || !out || (op == FMGI_UNIT_TRUNC_DIV && !b) ||
-        (op != FMGI_UNIT_SQRT && op != FMGI_UNIT_TRUNC_DIV))
+    if (!c || n < 0 || !a || !out || (op != FMGI_UNIT_SQRT && !b) ||
+        (op != FMGI_UNIT_SQRT && op != FMGI_UNIT_TRUNC_DIV && op != FMGI_UNIT_TRUNC_DIV_INV))
         return set_err(FMGI_ERR_ARG, "bad arguments");
     if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
     if (!n) return FMGI_OK;

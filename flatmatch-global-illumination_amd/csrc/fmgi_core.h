@@ -41,7 +41,7 @@ FMGI_HD f3 normalize3(f3 a) { return div3(a, len3(a)); }
  * reference Rectangle plus values photonmap.cl recomputes per test, hoisted to the host with the same
  * IEEE ops (bit-identical): wn = width/length(width) (photonmap.cl:145), wl = length(width) (:144),
  * hn/hl likewise (:149-150), and the sampler basis of the normal (bu, bv; photonmap.cl:65-70).
- * The last 8 words are the fast kernel's conservative filter constants (see fmgi_kernels.hip).
+ * iwl/ihl serve only tile_uv's fast path, which checks its result against a 2^-20 band.
  */
 struct __attribute__((aligned(16))) RectDev {
     float px, py, pz;      /* pos                      */
@@ -54,7 +54,8 @@ struct __attribute__((aligned(16))) RectDev {
     int32_t axis;          /* filter class: 0..5 = axis-aligned normal (+x,-x,+y,-y,+z,-z), -1 general */
     float bux, buy, buz;   /* sampler basis udir        */
     float bvx, bvy, bvz;   /* sampler basis vdir        */
-    float f[8];            /* filter constants          */
+    float iwl, ihl;        /* 1/wl, 1/hl correctly rounded (tile_uv's quotient estimate) */
+    float pad[6];
 };
 static_assert(sizeof(RectDev) == 128, "RectDev must be 128 B");
 
@@ -153,23 +154,29 @@ FMGI_HD float intersect_exact_uv(f3 n, f3 pos, f3 wn, float wl, f3 hn, float hl,
     return fac;
 }
 
-/* (int)(x / y) for 0 <= x / y < 2^30 (correctly rounded quotient, truncated). On the device: the
-   quotient through v_rcp_f32 is within 2^-21 relative of x / y and of its rounding, so when both ends of
-   the +-2^-20 band around it truncate to the same integer, that integer is the answer; otherwise (a
-   quotient next to an integer) the exact division decides. */
-FMGI_HD int trunc_div(float x, float y) {
+/* (int)(x / y) for 0 <= x / y < 2^30 (correctly rounded quotient, truncated), given iy ~ 1/y within
+   one ulp. On the device: x * iy is within 2^-21 relative of x / y and of its rounding, so when both
+   ends of the +-2^-20 band around it truncate to the same integer, that integer is the answer;
+   otherwise (a quotient next to an integer) the exact division decides. */
+FMGI_HD int trunc_div_inv(float x, float y, float iy) {
 #if defined(__HIP_DEVICE_COMPILE__)
-    const float q = x * __builtin_amdgcn_rcpf(y);
+    const float q = x * iy;
     const int lo = (int)(q * 0.99999904632568359375f), hi = (int)(q * 1.00000095367431640625f);
     if (lo == hi) return lo;
 #endif
     return (int)(x / y);
 }
 
-/* photonmap.cl:108-119: the tile of in-rect coordinates (dx, dy) */
-FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, int W, int H) {
-    int tx = trunc_div(dx * (float)W, wl);
-    int ty = trunc_div(dy * (float)H, hl);
+#if defined(__HIP_DEVICE_COMPILE__)
+FMGI_HD int trunc_div(float x, float y) { return trunc_div_inv(x, y, __builtin_amdgcn_rcpf(y)); }
+#else
+FMGI_HD int trunc_div(float x, float y) { return (int)(x / y); }
+#endif
+
+/* photonmap.cl:108-119: the tile of in-rect coordinates (dx, dy); iwl, ihl ~ 1/wl, 1/hl (one ulp) */
+FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, float iwl, float ihl, int W, int H) {
+    int tx = trunc_div_inv(dx * (float)W, wl, iwl);
+    int ty = trunc_div_inv(dy * (float)H, hl, ihl);
     tx = tx < 0 ? 0 : (tx > W - 1 ? W - 1 : tx);
     ty = ty < 0 ? 0 : (ty > H - 1 ? H - 1 : ty);
     return ty * W + tx;
@@ -178,7 +185,7 @@ FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, int W, int H) {
 /* photonmap.cl:95-120 */
 FMGI_HD int tile_at(f3 pos, f3 wn, float wl, f3 hn, float hl, int W, int H, f3 p) {
     f3 pDir = sub3(p, pos);
-    return tile_uv(dot3(wn, pDir), dot3(hn, pDir), wl, hl, W, H);
+    return tile_uv(dot3(wn, pDir), dot3(hn, pDir), wl, hl, 1.0f / wl, 1.0f / hl, W, H);
 }
 
 /* Warm-up skip-ahead (photonmap.cl:272-275): `r = rand()*40; for (i=0; i<r; i++) rand();` draws

@@ -76,7 +76,7 @@ __device__ __forceinline__ float exact_on(cptr<RectDev> R, int i, f3 src, f3 dir
 struct HitRec {
     int idx;             /* hit rect, or -1 (best = INFINITY: the photon escapes)          */
     float best, dx, dy;  /* exact hit distance and in-rect coordinates (photonmap.cl:99-100) */
-    float nx, ny, nz, wl, hl;
+    float nx, ny, nz, wl, hl, iwl, ihl;
     int base, W, H;
     float bux, buy, buz, bvx, bvy, bvz;
 };
@@ -87,6 +87,7 @@ __device__ __forceinline__ float exact_hit(const BakeArgs &a, int idx, f3 src, f
     h.idx = idx;
     h.nx = r.nx; h.ny = r.ny; h.nz = r.nz;
     h.wl = r.wl; h.hl = r.hl;
+    h.iwl = r.iwl; h.ihl = r.ihl;
     h.base = r.base; h.W = r.W; h.H = r.H;
     h.bux = r.bux; h.buy = r.buy; h.buz = r.buz;
     h.bvx = r.bvx; h.bvy = r.bvy; h.bvz = r.bvz;
@@ -776,7 +777,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         /* ---- stage 3: hit (photonmap.cl:216-258) ---- */
         pos = add3(pos, mul3(dir, h.best));
         const f3 hn = mkf3(h.nx, h.ny, h.nz);
-        const int texel = h.base + tile_uv(h.dx, h.dy, h.wl, h.hl, h.W, h.H); /* == tile_at(rect, pos) */
+        const int texel = h.base + tile_uv(h.dx, h.dy, h.wl, h.hl, h.iwl, h.ihl, h.W, h.H); /* == tile_at(rect, pos) */
         const bool last = depth + 1 == FMGI_MAX_DEPTH;
         /* (double)pos.z > 0.0005 (photonmap.cl:236) <=> pos.z > the largest float below 0.0005 */
         if (pos.z > 4.99999965541064739227294921875e-4f || rng_next(rng) > 0.75f) {
@@ -900,7 +901,8 @@ __global__ void k_unit(int op, const float *__restrict__ a, const float *__restr
                        int64_t n) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    out[i] = op == 0 ? __float_as_int(sqrt_cr(a[i])) : trunc_div(a[i], b[i]);
+    out[i] = op == 0 ? __float_as_int(sqrt_cr(a[i]))
+                     : (op == 1 ? trunc_div(a[i], b[i]) : trunc_div_inv(a[i], b[i], 1.0f / b[i]));
 }
 
 template <class Scan, class Acc>

@@ -57,6 +57,7 @@ __all__ = [
 
 UNIT_SQRT = 0       # fmgi_device_unit ops (include/flatmatch_gi.h)
 UNIT_TRUNC_DIV = 1
+UNIT_TRUNC_DIV_INV = 2
 
 
 def _ptr(a: np.ndarray | None):

@@ -263,9 +263,11 @@ void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);
 int fmgi_device_sincosf(fmgi_context *ctx, const float *x, float *s, float *c, int64_t n);
 /* Device arithmetic helpers of the bake kernel over n inputs (synchronous; for parity tests):
    op FMGI_UNIT_SQRT: out[i] = bits of the sampler's correctly rounded sqrtf(a[i]) (b unused);
-   op FMGI_UNIT_TRUNC_DIV: out[i] = (int)(a[i] / b[i]), the tile index step of photonmap.cl:108-109. */
+   op FMGI_UNIT_TRUNC_DIV: out[i] = (int)(a[i] / b[i]), the tile index step of photonmap.cl:108-109
+   (through v_rcp_f32); op FMGI_UNIT_TRUNC_DIV_INV: the same through the host-rounded 1.0f / b[i]. */
 #define FMGI_UNIT_SQRT 0
 #define FMGI_UNIT_TRUNC_DIV 1
+#define FMGI_UNIT_TRUNC_DIV_INV 2
 int fmgi_device_unit(fmgi_context *ctx, int op, const float *a, const float *b, int32_t *out, int64_t n);
 
 #ifdef __cplusplus

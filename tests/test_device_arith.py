@@ -59,5 +59,6 @@ def test_tile_trunc_div_near_every_integer(ctx):
     keep = (x / y) < 2.0**30
     x, y = x[keep], y[keep]
     want = np.trunc(x / y).astype(np.int64)  # float32 division: correctly rounded
-    got = ctx.device_unit(fmgi.UNIT_TRUNC_DIV, x, y)
-    assert np.array_equal(got.astype(np.int64), want)
+    for op in (fmgi.UNIT_TRUNC_DIV, fmgi.UNIT_TRUNC_DIV_INV):
+        got = ctx.device_unit(op, x, y)
+        assert np.array_equal(got.astype(np.int64), want), op
