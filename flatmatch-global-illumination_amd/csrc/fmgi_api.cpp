@@ -942,6 +942,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
     const int block = 256;
+    fmgi_bake_lds(kernel, c->accum, block, a.fimg_bytes, &a.ring_off);
     if (c->accum != FMGI_ACCUM_STREAM) {
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;

@@ -82,6 +82,7 @@ struct BakeArgs {
     uint64_t stream_cap;
     unsigned long long *stream_cursor;
     unsigned long long *overflow; /* set if a reservation would pass stream_cap (never, by sizing) */
+    int ring_off;                 /* byte offset of the per-wave code rings in dynamic LDS (fmgi_bake_lds) */
     int num_texels;
     /* debug trace (TRACE kernels only) */
     void *events;                  /* fmgi_event[(item - item_begin) * 800 + k]                     */
@@ -94,6 +95,8 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 
 /* stream accumulation geometry (fmgi_accum.hip) */
 #define FMGI_STREAM_BLOCK 4096 /* codes reserved per wave at a time                         */
+#define FMGI_RING_CODES 1024   /* codes a wave collects in LDS before writing them out       */
+static_assert(FMGI_STREAM_BLOCK % FMGI_RING_CODES == 0, "ring flushes must tile the stream blocks");
 #define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
 #define FMGI_TILE_BITS 12      /* 4096-texel tiles summed in LDS                              */
 #define FMGI_MAX_TILES 1024    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */
@@ -117,6 +120,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);
+size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off);
 hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long *colfx, unsigned long long *lm,
                                      int n, hipStream_t s);
 hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long *src, int64_t n, hipStream_t s);

@@ -587,28 +587,23 @@ struct AccNone {
 
 /* Deposits become codes (texel << 10 | colour state) appended to a stream (fmgi_accum.hip folds it).
    The append is a wave-level operation at the end of each loop iteration, where every live lane of the
-   wave is active: the depositing lanes get consecutive slots (ballot + mbcnt), so one iteration's codes
-   are one coalesced store; one lane reserves a new FMGI_STREAM_BLOCK-code block when the current one
-   fills (the wave-uniform [wbase, wend) is kept identical in every live lane). */
+   wave is active: the depositing lanes get consecutive slots (ballot + mbcnt) in the wave's LDS ring
+   (FMGI_RING_CODES + 64 codes), and every time the ring holds FMGI_RING_CODES codes the wave copies them
+   to its block of the global stream with 16-B stores. A store per iteration would put its completion
+   into the next iteration's s_waitcnt vmcnt (gfx9 counts stores there): the ring makes that one flush per
+   ~16 iterations. Global blocks are FMGI_STREAM_BLOCK codes (a multiple of the ring), reserved by one
+   lane with an atomic, so a flush always fits the block it starts in. `tot` (codes appended by the wave)
+   is monotonic: after the loop the lane that left last holds the current state (finish). */
 struct WaveStream {
-    uint64_t base = 0, end = 0;
+    uint64_t base = 0, end = 0; /* free part of the wave's current global block */
+    uint32_t tot = 0;           /* codes appended; the ring holds tot % FMGI_RING_CODES of them */
 };
 
 struct AccStream {
     static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
-    static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, bool dep, uint32_t code) {
-        const uint64_t m = __ballot(dep);
-        if (m == 0) return;
-        const uint32_t n = (uint32_t)__popcll(m);
-        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
-        const uint64_t room = ws.end - ws.base;
-        if (n <= room) {
-            if (dep) a.stream[ws.base + r] = code;
-            ws.base += n;
-            return;
-        }
-        if (dep && r < room) a.stream[ws.base + r] = code;
-        /* one lane reserves the next block; every live lane learns its base */
+
+    /* a fresh global block for the wave (every live lane learns it) */
+    static __device__ __forceinline__ void reserve(const BakeArgs &a, WaveStream &ws) {
         const uint64_t live = __ballot(true);
         const int leader = __ffsll((long long)live) - 1;
         unsigned long long nb = 0;
@@ -620,19 +615,58 @@ struct AccStream {
         ws.base = nb;
         ws.end = nb + FMGI_STREAM_BLOCK;
         if (ws.end > a.stream_cap) ws.end = ws.base; /* (never by sizing) drop instead of writing out of bounds */
-        if (dep && r >= room && ws.base + (r - room) < ws.end) a.stream[ws.base + (r - room)] = code;
-        ws.base += n - room;
-        if (ws.base > ws.end) ws.base = ws.end;
     }
-    /* after the loop (all lanes of the wave reconverged): pad the wave's last block with sentinels */
-    static __device__ __forceinline__ void finish(const BakeArgs &a, WaveStream &ws) {
-        uint64_t b = ws.base, e = ws.end;
-        for (int off = 32; off > 0; off >>= 1) { /* lanes that left early hold older (smaller) values */
-            const uint64_t ob = __shfl_xor(b, off, 64), oe = __shfl_xor(e, off, 64);
-            b = ob > b ? ob : b;
-            e = oe > e ? oe : e;
+
+    /* copy ring[0, n) (n <= FMGI_RING_CODES, a multiple of 4) to the block, 16 B per live lane per step */
+    static __device__ __forceinline__ void copy_out(const BakeArgs &a, WaveStream &ws, const uint32_t *ring,
+                                                    uint32_t n) {
+        if (ws.end - ws.base < n) reserve(a, ws);
+        if (ws.end - ws.base < n) return; /* overflow (counted in reserve) */
+        const uint64_t live = __ballot(true);
+        const uint32_t nl = (uint32_t)__popcll(live);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+        uint4 *dst = (uint4 *)(a.stream + ws.base);
+        for (uint32_t k = r; k < n / 4; k += nl) dst[k] = ((const uint4 *)ring)[k];
+        ws.base += n;
+    }
+
+    static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, uint32_t *ring, bool dep,
+                                                  uint32_t code) {
+        const uint64_t m = __ballot(dep);
+        if (m == 0) return;
+        const uint32_t n = (uint32_t)__popcll(m);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t fill = ws.tot % FMGI_RING_CODES;
+        if (dep) ring[fill + r] = code;
+        ws.tot += n;
+        if (fill + n < FMGI_RING_CODES) return;
+        /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
+        copy_out(a, ws, ring, FMGI_RING_CODES);
+        const uint32_t rest = fill + n - FMGI_RING_CODES; /* < n <= live lanes: one code per live lane */
+        const uint64_t live = __ballot(true);
+        const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+        const uint32_t v = k < rest ? ring[FMGI_RING_CODES + k] : 0u;
+        if (k < rest) ring[k] = v;
+    }
+
+    /* after the loop (all lanes of the wave reconverged): take the state of the lane that appended last,
+       write out the ring's remaining codes (padded to 16 B with sentinels) and fill the rest of the
+       block with sentinels */
+    static __device__ __forceinline__ void finish(const BakeArgs &a, WaveStream &ws, uint32_t *ring) {
+        uint32_t mx = ws.tot;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint32_t o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
         }
-        for (uint64_t k = b + __lane_id(); k < e; k += 64) a.stream[k] = 0xFFFFFFFFu;
+        const int src = __ffsll((long long)__ballot(ws.tot == mx)) - 1;
+        ws.tot = __shfl(ws.tot, src, 64);
+        ws.base = __shfl(ws.base, src, 64);
+        ws.end = __shfl(ws.end, src, 64);
+        const uint32_t fill = ws.tot % FMGI_RING_CODES, padded = (fill + 3) & ~3u;
+        const uint32_t lane = __lane_id();
+        for (uint32_t k = fill + lane; k < padded; k += 64) ring[k] = 0xFFFFFFFFu;
+        if (padded) copy_out(a, ws, ring, padded);
+        for (uint64_t k = ws.base + lane; k < ws.end; k += 64) a.stream[k] = 0xFFFFFFFFu;
     }
 };
 
@@ -684,6 +718,8 @@ __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
 template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
+    /* AccStream: this wave's ring of deposit codes, after the scan image in LDS */
+    uint32_t *const ring = (uint32_t *)(s_img + a.ring_off) + (threadIdx.x >> 6) * (FMGI_RING_CODES + 64);
     if (Scan::kLds) { /* stage the filter image once per workgroup */
         const int n16 = a.fimg_bytes >> 4;
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
@@ -818,10 +854,10 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         depth++;
         }
         sst.clk.lap(ST_HIT);
-        if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, dep, code);
+        if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, ring, dep, code);
         sst.clk.lap(ST_APPEND);
     }
-    if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws);
+    if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws, ring);
     if (TRACE && photon >= 0) {
         a.ev_counts[item - a.item_begin] = nev;
         a.rng_final[item - a.item_begin] = rng;
@@ -939,10 +975,18 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
 
 } // namespace
 
+/* dynamic LDS of a bake launch: the scan image (fast / grid scans), then one ring per wave (AccStream) */
+size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
+    const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
+    if (ring_off) *ring_off = (int)img;
+    return img + (accum == 4 ? (size_t)(block / 64) * (FMGI_RING_CODES + 64) * 4 : 0);
+}
+
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes) {
     int n = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bake_kernel(kernel, accum, trace), block,
-                                                     kernel != 0 ? (size_t)lds_bytes : 0) != hipSuccess)
+                                                     fmgi_bake_lds(kernel, accum, block, lds_bytes, nullptr)) !=
+        hipSuccess)
         return 0;
     return n;
 }
@@ -950,7 +994,9 @@ int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int 
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s) {
     dim3 grid(grid_blocks), blk(block);
-    const size_t lds = kernel != 0 ? (size_t)a.fimg_bytes : 0;
+    int ring_off = 0;
+    const size_t lds = fmgi_bake_lds(kernel, accum, block, a.fimg_bytes, &ring_off);
+    if (ring_off != a.ring_off) return hipErrorInvalidValue; /* the caller sets a.ring_off from fmgi_bake_lds */
     if (kernel == 2) { /* FMGI_KERNEL_GRID */
         if (accum == 2) launch3<ScanGrid, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanGrid, AccNone>(a, trace, grid, blk, lds, s);
