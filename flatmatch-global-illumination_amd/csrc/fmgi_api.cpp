@@ -941,7 +941,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.ev_counts = counts;
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
-    const int block = 256;
+    int block = 256;
+    if (const char *be = getenv("FMGI_BLOCK")) /* experiments: 64..1024 lanes per workgroup */
+        if (atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) block = atoi(be);
     fmgi_bake_lds(kernel, c->accum, block, a.fimg_bytes, &a.ring_off);
     if (c->accum != FMGI_ACCUM_STREAM) {
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
