@@ -8,7 +8,7 @@
  *
  *   bake : each deposit appends a 32-bit code (texel << 10 | colour state) to a stream with plain,
  *          wave-coalesced stores (k_bake, AccStream; one reservation atomic per 4096 codes per wave)
- *   sort : per 8192-code slice, a counting sort by 4096-texel tile in LDS, written back contiguously,
+ *   sort : per 8192-code slice, a counting sort by 2048-texel tile in LDS, written back contiguously,
  *          plus the slice's tile offsets (u16)                                         k_slice_sort
  *   sum  : one workgroup per (tile, group of slices) reads that tile's run of every slice of its group
  *          and sums it exactly in LDS (int64 R, G - R, B - R per texel, ds_add_u64: a grey deposit
@@ -155,7 +155,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
     const uint64_t nslices = (sb.cap + kSlice - 1) / kSlice;
     hipLaunchKernelGGL(k_slice_sort, dim3((unsigned)nslices), dim3(256), 0, s, sb.stream, sb.cursor, sb.cap, P,
                        sb.sorted, sb.toff);
-    const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 112 KiB of the 160 */
+    const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 64 KiB: two workgroups per CU */
     static bool lds_set = false;
     if (!lds_set) {
         hipError_t e = hipFuncSetAttribute((const void *)k_tile_runs, hipFuncAttributeMaxDynamicSharedMemorySize,
