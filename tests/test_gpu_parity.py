@@ -104,6 +104,23 @@ def test_per_photon_traces_boxes(torch_cuda, box200, box2000, offsets, kernel):
         ctx.close()
 
 
+def test_box_traces_without_axes_mode(torch_cuda, box200, offsets):
+    """The closed boxes use ScanGrid's one-plane-per-class phase 1; FMGI_NO_AXES=1 routes them through
+    the sorted <= 4-slot phase 1 instead, which no other scene here reaches: same traces."""
+    os.environ["FMGI_NO_AXES"] = "1"
+    try:
+        spa = 172_413_793
+        L = _oracle_plan(box200, spa, offsets)
+        ctx = _ctx(box200, spa, offsets)
+        _compare_traces(box200, ctx, L, 3000, 3128, fmgi.KERNEL_GRID)
+        lm = _bake_gpu(torch_cuda, ctx, 5_000, 25_000, fmgi.KERNEL_GRID)
+        olm, _ = O.bake(box200, L, 5_000, 25_000)
+        assert np.array_equal(lm[:, :3], olm)
+        ctx.close()
+    finally:
+        os.environ.pop("FMGI_NO_AXES", None)
+
+
 ACCUMS = [fmgi.ACCUM_FX3, fmgi.ACCUM_STATE, fmgi.ACCUM_STREAM]
 
 
