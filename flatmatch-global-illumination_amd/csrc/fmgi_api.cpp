@@ -427,6 +427,7 @@ struct fmgi_context {
     int32_t *d_src_launch0 = nullptr;     /* [nsrc]     */
     unsigned long long *d_counter = nullptr;
     unsigned long long *d_stats = nullptr;
+    FmgiSinCosCoef *d_sincos = nullptr; /* the samplers' double constants (BakeArgs::sincos) */
     /* ScanFast filter image + non-axis-aligned rect list */
     FilterRec *d_fimg = nullptr;
     int fimg_bytes = 0;
@@ -503,6 +504,8 @@ FMGI_API fmgi_context *fmgi_create(int device) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_counter, 64) != hipSuccess ||
         hipMalloc(&c->d_stats, KSTAT_ALLOC * sizeof(unsigned long long)) != hipSuccess ||
+        hipMalloc(&c->d_sincos, sizeof(FmgiSinCosCoef)) != hipSuccess ||
+        hipMemcpy(c->d_sincos, &kFmgiSinCos, sizeof(FmgiSinCosCoef), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(c->d_stats, 0, KSTAT_ALLOC * sizeof(unsigned long long)) != hipSuccess) {
         set_err(FMGI_ERR_HIP, "context allocation failed on device %d", device);
         fmgi_destroy(c);
@@ -548,6 +551,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_colpack);
     hipFree(c->d_counter);
     hipFree(c->d_stats);
+    hipFree(c->d_sincos);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -941,6 +945,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.ev_counts = counts;
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
+    a.sincos = c->d_sincos;
     int block = 256;
     if (const char *be = getenv("FMGI_BLOCK")) /* experiments: 64..1024 lanes per workgroup */
         if (atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) block = atoi(be);
@@ -1172,7 +1177,7 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
     float *d = nullptr;
     HIPCHK(hipMalloc(&d, (size_t)n * 12));
     hipError_t err = hipMemcpy(d, x, (size_t)n * 4, hipMemcpyHostToDevice);
-    if (err == hipSuccess) err = fmgi_launch_sincos(d, d + n, d + 2 * n, n, c->stream);
+    if (err == hipSuccess) err = fmgi_launch_sincos(d, d + n, d + 2 * n, n, c->d_sincos, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     if (err == hipSuccess) err = hipMemcpy(s, d + n, (size_t)n * 4, hipMemcpyDeviceToHost);
     if (err == hipSuccess) err = hipMemcpy(co, d + 2 * n, (size_t)n * 4, hipMemcpyDeviceToHost);

@@ -108,12 +108,14 @@ FMGI_HD float sqrt_cr(float x) {
 #endif
 }
 
-/* photonmap.cl:27-74 with the basis precomputed: fold=1 is the window ("sky") sampler. */
-FMGI_HD f3 sample_dir(uint32_t &rng, f3 n, f3 bu, f3 bv, bool fold) {
+/* photonmap.cl:27-74 with the basis precomputed: fold=1 is the window ("sky") sampler. k points at
+   the sin/cos constants (fmgi_math.h). */
+template <class K>
+FMGI_HD f3 sample_dir(uint32_t &rng, f3 n, f3 bu, f3 bv, bool fold, const K &k) {
     float r = sqrt_cr(rng_next(rng));
     float phi = 6.283184f * rng_next(rng);
     float sn, cs;
-    fmgi_sincosf(phi, &sn, &cs);
+    fmgi_sincosf_k(phi, k, &sn, &cs);
     float u = r * cs;
     float v = r * sn;
     float w = sqrt_cr(1.0f - r * r);

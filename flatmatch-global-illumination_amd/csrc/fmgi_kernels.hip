@@ -725,6 +725,8 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
         __syncthreads();
     }
+    /* sin/cos constants through a scalar pointer, not as literals (fmgi_math.h) */
+    const cptr<FmgiSinCosCoef> K = (cptr<FmgiSinCosCoef>)a.sincos;
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
@@ -782,7 +784,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
             n_ph++;
         }
         sst.clk.lap(ST_START);
-        if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
+        if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win, K);
         if (start) {
             const SrcDev &S = a.srcs[srci];
             pos = add3(add3(add3(mkf3(S.px, S.py, S.pz), mul3(mkf3(S.wx, S.wy, S.wz), edx)),
@@ -923,11 +925,13 @@ __global__ void k_add_u64(unsigned long long *__restrict__ dst, const unsigned l
     if (i < n) dst[i] += src[i];
 }
 
-__global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, float *__restrict__ c, int64_t n) {
+__global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, float *__restrict__ c, int64_t n,
+                         const FmgiSinCosCoef *coef) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
+    const cptr<FmgiSinCosCoef> K = (cptr<FmgiSinCosCoef>)coef; /* as k_bake reads them */
     float a, b;
-    fmgi_sincosf(x[i], &a, &b);
+    fmgi_sincosf_k(x[i], K, &a, &b);
     s[i] = a;
     c[i] = b;
 }
@@ -1043,9 +1047,10 @@ hipError_t fmgi_launch_unit(int op, const float *a, const float *b, int32_t *out
     return hipGetLastError();
 }
 
-hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, hipStream_t s) {
+hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, const FmgiSinCosCoef *coef,
+                              hipStream_t s) {
     if (n <= 0) return hipSuccess;
     int64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_sincos, dim3((unsigned)blocks), dim3(256), 0, s, x, sn, cs, n);
+    hipLaunchKernelGGL(k_sincos, dim3((unsigned)blocks), dim3(256), 0, s, x, sn, cs, n, coef);
     return hipGetLastError();
 }

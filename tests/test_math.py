@@ -16,7 +16,7 @@ from conftest import PKG, REPO
 def test_sincos_exhaustive_vs_glibc(tmp_path):
     exe = tmp_path / "check_sincos"
     subprocess.run(
-        ["gcc", "-O2", "-ffp-contract=off", "-fopenmp", "-I", os.path.join(PKG, "csrc"),
+        ["g++", "-x", "c++", "-O2", "-ffp-contract=off", "-fopenmp", "-I", os.path.join(PKG, "csrc"),
          os.path.join(REPO, "tests", "tools", "check_sincos.c"), "-o", str(exe), "-lm"],
         check=True,
     )
