@@ -64,30 +64,22 @@ namespace {
 
 f3 v3of(const fmgi_vec3 &v) { return mkf3(v.s[0], v.s[1], v.s[2]); }
 
-/* Host restatement of the per-rectangle values photonmap.cl recomputes per test (bit-identical). */
+/* A wall as the kernels read it: the reference Rectangle's fields; the values photonmap.cl derives from
+   them with OpenCL builtins (lengths, unit edges, sampler basis) are filled in on the device by
+   k_scene_setup, so they carry exactly the builtins' gfx950 bits. */
 RectDev make_rect(const fmgi_rect &r) {
     RectDev d;
     memset(&d, 0, sizeof d);
-    f3 pos = v3of(r.pos), w = v3of(r.width), h = v3of(r.height), n = v3of(r.n);
-    d.px = pos.x; d.py = pos.y; d.pz = pos.z;
-    d.nx = n.x; d.ny = n.y; d.nz = n.z;
-    float wl = len3(w), hl = len3(h);
-    f3 wn = div3(w, wl), hn = div3(h, hl);
-    d.wnx = wn.x; d.wny = wn.y; d.wnz = wn.z; d.wl = wl;
-    d.hnx = hn.x; d.hny = hn.y; d.hnz = hn.z; d.hl = hl;
-    d.iwl = 1.0f / wl;
-    d.ihl = 1.0f / hl;
+    d.px = r.pos.s[0]; d.py = r.pos.s[1]; d.pz = r.pos.s[2];
+    d.nx = r.n.s[0]; d.ny = r.n.s[1]; d.nz = r.n.s[2];
     d.base = r.lightmapSetup[0];
     d.W = r.lightmapSetup[1];
     d.H = r.lightmapSetup[2];
-    f3 bu, bv;
-    sampler_basis(n, bu, bv);
-    d.bux = bu.x; d.buy = bu.y; d.buz = bu.z;
-    d.bvx = bv.x; d.bvy = bv.y; d.bvz = bv.z;
     d.axis = -1;
     return d;
 }
 
+/* An emitter (window or light); its sampler basis comes from k_scene_setup as well. */
 SrcDev make_src(const fmgi_rect &r) {
     SrcDev s;
     memset(&s, 0, sizeof s);
@@ -95,17 +87,13 @@ SrcDev make_src(const fmgi_rect &r) {
     s.wx = r.width.s[0]; s.wy = r.width.s[1]; s.wz = r.width.s[2];
     s.hx = r.height.s[0]; s.hy = r.height.s[1]; s.hz = r.height.s[2];
     s.nx = r.n.s[0]; s.ny = r.n.s[1]; s.nz = r.n.s[2];
-    f3 bu, bv;
-    sampler_basis(v3of(r.n), bu, bv);
-    s.bux = bu.x; s.buy = bu.y; s.buz = bu.z;
-    s.bvx = bv.x; s.bvy = bv.y; s.bvz = bv.z;
     return s;
 }
 
 /* global_illumination_cl.c:217-222: area in float, (float)spa*area/100 -> uint64, then
    (n / wg + 1) * wg (always at least one extra work group, as the reference does). */
 uint64_t source_items(const fmgi_rect &src, float spa, uint64_t wg) {
-    float area = len3(v3of(src.width)) * len3(v3of(src.height));
+    float area = host_len3(v3of(src.width)) * host_len3(v3of(src.height));
     uint64_t n = (uint64_t)((spa * area) / 100);
     return (n / wg + 1) * wg;
 }
@@ -427,7 +415,6 @@ struct fmgi_context {
     int32_t *d_src_launch0 = nullptr;     /* [nsrc]     */
     unsigned long long *d_counter = nullptr;
     unsigned long long *d_stats = nullptr;
-    FmgiSinCosCoef *d_sincos = nullptr; /* the samplers' double constants (BakeArgs::sincos) */
     /* ScanFast filter image + non-axis-aligned rect list */
     FilterRec *d_fimg = nullptr;
     int fimg_bytes = 0;
@@ -504,8 +491,6 @@ FMGI_API fmgi_context *fmgi_create(int device) {
     if (hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking) != hipSuccess ||
         hipMalloc(&c->d_counter, 64) != hipSuccess ||
         hipMalloc(&c->d_stats, KSTAT_ALLOC * sizeof(unsigned long long)) != hipSuccess ||
-        hipMalloc(&c->d_sincos, sizeof(FmgiSinCosCoef)) != hipSuccess ||
-        hipMemcpy(c->d_sincos, &kFmgiSinCos, sizeof(FmgiSinCosCoef), hipMemcpyHostToDevice) != hipSuccess ||
         hipMemset(c->d_stats, 0, KSTAT_ALLOC * sizeof(unsigned long long)) != hipSuccess) {
         set_err(FMGI_ERR_HIP, "context allocation failed on device %d", device);
         fmgi_destroy(c);
@@ -551,7 +536,6 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_colpack);
     hipFree(c->d_counter);
     hipFree(c->d_stats);
-    hipFree(c->d_sincos);
     if (c->stream) hipStreamDestroy(c->stream);
     delete c;
 }
@@ -714,6 +698,21 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     if (!sd.empty()) {
         HIPCHK(hipMalloc(&c->d_srcs, sd.size() * sizeof(SrcDev)));
         HIPCHK(hipMemcpy(c->d_srcs, sd.data(), sd.size() * sizeof(SrcDev), hipMemcpyHostToDevice));
+    }
+    {   /* the builtin-derived per-rect / per-emitter values, on the device (k_scene_setup) */
+        std::vector<fmgi_rect> raw(walls, walls + num_walls);
+        raw.insert(raw.end(), c->h_srcs.begin(), c->h_srcs.end());
+        if (!raw.empty()) {
+            fmgi_rect *d_raw = nullptr;
+            HIPCHK(hipMalloc(&d_raw, raw.size() * sizeof(fmgi_rect)));
+            hipError_t e = hipMemcpy(d_raw, raw.data(), raw.size() * sizeof(fmgi_rect), hipMemcpyHostToDevice);
+            if (e == hipSuccess)
+                e = fmgi_launch_scene_setup(d_raw, num_walls, d_raw + num_walls, (int)c->h_srcs.size(), c->d_rects,
+                                            c->d_srcs, c->stream);
+            if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
+            hipFree(d_raw);
+            if (e != hipSuccess) return set_err(FMGI_ERR_HIP, "scene setup: %s", hipGetErrorString(e));
+        }
     }
     hipFree(c->d_fimg);
     hipFree(c->d_general);
@@ -945,7 +944,6 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.ev_counts = counts;
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
-    a.sincos = c->d_sincos;
     int block = 256;
     if (const char *be = getenv("FMGI_BLOCK")) /* experiments: 64..1024 lanes per workgroup */
         if (atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) block = atoi(be);
@@ -1169,7 +1167,7 @@ FMGI_API int fmgi_trace_items(fmgi_context *c, uint64_t b, uint64_t e, int kerne
     return rc;
 }
 
-FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, float *co, int64_t n) {
+static int device_sincos(fmgi_context *c, const float *x, float *s, float *co, int64_t n, int lib) {
     if (!c || n < 0) return set_err(FMGI_ERR_ARG, "bad arguments");
     if (c->device == FMGI_HOST_ONLY) return set_err(FMGI_ERR_NO_DEVICE, "host-only context");
     if (!n) return FMGI_OK;
@@ -1177,13 +1175,21 @@ FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, floa
     float *d = nullptr;
     HIPCHK(hipMalloc(&d, (size_t)n * 12));
     hipError_t err = hipMemcpy(d, x, (size_t)n * 4, hipMemcpyHostToDevice);
-    if (err == hipSuccess) err = fmgi_launch_sincos(d, d + n, d + 2 * n, n, c->d_sincos, c->stream);
+    if (err == hipSuccess) err = fmgi_launch_sincos(d, d + n, d + 2 * n, n, lib, c->stream);
     if (err == hipSuccess) err = hipStreamSynchronize(c->stream);
     if (err == hipSuccess) err = hipMemcpy(s, d + n, (size_t)n * 4, hipMemcpyDeviceToHost);
     if (err == hipSuccess) err = hipMemcpy(co, d + 2 * n, (size_t)n * 4, hipMemcpyDeviceToHost);
     hipFree(d);
     if (err != hipSuccess) return set_err(FMGI_ERR_HIP, "device sincos: %s", hipGetErrorString(err));
     return FMGI_OK;
+}
+
+FMGI_API int fmgi_device_sincosf(fmgi_context *c, const float *x, float *s, float *co, int64_t n) {
+    return device_sincos(c, x, s, co, n, 0);
+}
+
+FMGI_API int fmgi_device_sincosf_library(fmgi_context *c, const float *x, float *s, float *co, int64_t n) {
+    return device_sincos(c, x, s, co, n, 1);
 }
 
 FMGI_API int fmgi_device_unit(fmgi_context *c, int op, const float *a, const float *b, int32_t *out, int64_t n) {

@@ -2,9 +2,9 @@
  * fmgi_core.h -- device-side data layout and the exact photon-step arithmetic.
  *
  * Everything in this header is evaluated with IEEE fp32 ops in the order of photonmap.cl
- * (this translation unit is compiled with -ffp-contract=off and correctly rounded div/sqrt), so the
- * results are bit-identical to the oracle contract (oracle/fm_oracle.h). It is shared by the exact
- * kernel, the fast kernel's verification step and the host-side precomputation.
+ * (this translation unit is compiled with -ffp-contract=off and correctly rounded div/sqrt) and the
+ * OpenCL builtins as ROCm implements them for gfx950, so the results are bit-identical to the oracle
+ * contract (oracle/fm_oracle.h) and to the reference kernel built for MI355X.
  */
 #ifndef FMGI_CORE_H
 #define FMGI_CORE_H
@@ -30,17 +30,21 @@ FMGI_HD f3 add3(f3 a, f3 b) { return mkf3(a.x + b.x, a.y + b.y, a.z + b.z); }
 FMGI_HD f3 sub3(f3 a, f3 b) { return mkf3(a.x - b.x, a.y - b.y, a.z - b.z); }
 FMGI_HD f3 mul3(f3 a, float s) { return mkf3(a.x * s, a.y * s, a.z * s); }
 FMGI_HD f3 div3(f3 a, float s) { return mkf3(a.x / s, a.y / s, a.z / s); }
-/* OpenCL dot/cross/length/normalize as fixed by the parity contract */
-FMGI_HD float dot3(f3 a, f3 b) { float t = a.x * b.x; t = t + a.y * b.y; return t + a.z * b.z; }
-FMGI_HD f3 cross3(f3 a, f3 b) { return mkf3(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x); }
-FMGI_HD float len3(f3 a) { return sqrtf(dot3(a, a)); }
-FMGI_HD f3 normalize3(f3 a) { return div3(a, len3(a)); }
+/* OpenCL dot and cross as ROCm's device library defines them (opencl.bc; its llvm.fmuladd is an FMA on
+   gfx950): what the reference kernel computes on MI355X */
+FMGI_HD float dot3(f3 a, f3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+FMGI_HD f3 cross3(f3 a, f3 b) {
+    return mkf3(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+/* the reference HOST's length() (vector3_cl.c:93, gcc without FMA): the launch schedule's source area */
+FMGI_HD float host_len3(f3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
 
 /*
  * One wall rectangle as the kernels read it: 128 B (two s_load_dwordx16). Exact fields are the
- * reference Rectangle plus values photonmap.cl recomputes per test, hoisted to the host with the same
- * IEEE ops (bit-identical): wn = width/length(width) (photonmap.cl:145), wl = length(width) (:144),
- * hn/hl likewise (:149-150), and the sampler basis of the normal (bu, bv; photonmap.cl:65-70).
+ * reference Rectangle plus values photonmap.cl recomputes per test, hoisted out of the loop and computed
+ * once per scene on the device with the same builtins (k_scene_setup, bit-identical): wn =
+ * width/length(width) (photonmap.cl:145), wl = length(width) (:144), hn/hl likewise (:149-150), and the
+ * sampler basis of the normal (bu, bv; photonmap.cl:65-70).
  * iwl/ihl serve only tile_uv's fast path, which checks its result against a 2^-20 band.
  */
 struct __attribute__((aligned(16))) RectDev {
@@ -82,16 +86,6 @@ FMGI_HD float rng_next(uint32_t &s) {
     return (float)s * 2.3283064365386963e-10f; /* == (float)s / (float)0xFFFFFFFF, an exact 2^-32 scale */
 }
 
-/* Sampler basis for a normal: photonmap.cl:43-48 (== :65-70). Host-side precomputation. */
-FMGI_HD void sampler_basis(f3 n, f3 &bu, f3 &bv) {
-    f3 udir = mkf3(0, 0, 1);
-    if (fabsf(dot3(udir, n)) >= 0.999999f) udir = mkf3(0, 1, 0);
-    f3 vdir = normalize3(cross3(udir, n));
-    udir = normalize3(cross3(vdir, n));
-    bu = udir;
-    bv = vdir;
-}
-
 /* Correctly rounded sqrtf (== sqrtf bit for bit) for x == 0 and 2^-96 <= x < inf: v_sqrt_f32 plus one
    residual correction, i.e. LLVM's gfx9 expansion without its rescaling of tiny inputs. The samplers'
    arguments are rand() in {0} u [2^-32, 1] and 1 - r*r in {0} u [2^-24, 1]. */
@@ -108,14 +102,12 @@ FMGI_HD float sqrt_cr(float x) {
 #endif
 }
 
-/* photonmap.cl:27-74 with the basis precomputed: fold=1 is the window ("sky") sampler. k points at
-   the sin/cos constants (fmgi_math.h). */
-template <class K>
-FMGI_HD f3 sample_dir(uint32_t &rng, f3 n, f3 bu, f3 bv, bool fold, const K &k) {
+/* photonmap.cl:27-74 with the basis precomputed (k_scene_setup): fold=1 is the window ("sky") sampler */
+FMGI_HD f3 sample_dir(uint32_t &rng, f3 n, f3 bu, f3 bv, bool fold) {
     float r = sqrt_cr(rng_next(rng));
     float phi = 6.283184f * rng_next(rng);
     float sn, cs;
-    fmgi_sincosf_k(phi, k, &sn, &cs);
+    fmgi_sincosf(phi, &sn, &cs);
     float u = r * cs;
     float v = r * sn;
     float w = sqrt_cr(1.0f - r * r);
@@ -182,12 +174,6 @@ FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, float iwl, float ihl
     tx = tx < 0 ? 0 : (tx > W - 1 ? W - 1 : tx);
     ty = ty < 0 ? 0 : (ty > H - 1 ? H - 1 : ty);
     return ty * W + tx;
-}
-
-/* photonmap.cl:95-120 */
-FMGI_HD int tile_at(f3 pos, f3 wn, float wl, f3 hn, float hl, int W, int H, f3 p) {
-    f3 pDir = sub3(p, pos);
-    return tile_uv(dot3(wn, pDir), dot3(hn, pDir), wl, hl, 1.0f / wl, 1.0f / hl, W, H);
 }
 
 /* Warm-up skip-ahead (photonmap.cl:272-275): `r = rand()*40; for (i=0; i<r; i++) rand();` draws

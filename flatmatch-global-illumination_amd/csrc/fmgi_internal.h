@@ -83,7 +83,6 @@ struct BakeArgs {
     unsigned long long *stream_cursor;
     unsigned long long *overflow; /* set if a reservation would pass stream_cap (never, by sizing) */
     int ring_off;                 /* byte offset of the per-wave code rings in dynamic LDS (fmgi_bake_lds) */
-    const FmgiSinCosCoef *sincos; /* the sampler's double constants in device memory (scalar loads) */
     int num_texels;
     /* debug trace (TRACE kernels only) */
     void *events;                  /* fmgi_event[(item - item_begin) * 800 + k]                     */
@@ -128,8 +127,10 @@ hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long
 hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long *src, int64_t n, hipStream_t s);
 hipError_t fmgi_launch_finalize(const unsigned long long *lm, const float *tin, float *tout, int64_t n,
                                 hipStream_t s);
-hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, const FmgiSinCosCoef *coef,
-                              hipStream_t s);
+hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, int lib, hipStream_t s);
+struct fmgi_rect;
+hipError_t fmgi_launch_scene_setup(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, int ns, RectDev *rd,
+                                   SrcDev *sd, hipStream_t s);
 hipError_t fmgi_launch_unit(int op, const float *a, const float *b, int32_t *out, int64_t n, hipStream_t s);
 
 #endif

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "fmgi_internal.h"
+#include "flatmatch_gi.h"
 
 #if defined(__clang__)
 #pragma clang fp contract(off)
@@ -725,8 +726,6 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
         __syncthreads();
     }
-    /* sin/cos constants through a scalar pointer, not as literals (fmgi_math.h) */
-    const cptr<FmgiSinCosCoef> K = (cptr<FmgiSinCosCoef>)a.sincos;
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
@@ -784,7 +783,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
             n_ph++;
         }
         sst.clk.lap(ST_START);
-        if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win, K);
+        if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
         if (start) {
             const SrcDev &S = a.srcs[srci];
             pos = add3(add3(add3(mkf3(S.px, S.py, S.pz), mul3(mkf3(S.wx, S.wy, S.wz), edx)),
@@ -925,15 +924,104 @@ __global__ void k_add_u64(unsigned long long *__restrict__ dst, const unsigned l
     if (i < n) dst[i] += src[i];
 }
 
-__global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, float *__restrict__ c, int64_t n,
-                         const FmgiSinCosCoef *coef) {
+/* the samplers' sin/cos over n inputs: the restatement (fmgi_math.h) or, lib = 1, the device library's
+   sinf/cosf it restates (parity tests) */
+__global__ void k_sincos(const float *__restrict__ x, float *__restrict__ s, float *__restrict__ c, int64_t n, int lib) {
     int64_t i = (int64_t)blockIdx.x * blockDim.x + threadIdx.x;
     if (i >= n) return;
-    const cptr<FmgiSinCosCoef> K = (cptr<FmgiSinCosCoef>)coef; /* as k_bake reads them */
     float a, b;
-    fmgi_sincosf_k(x[i], K, &a, &b);
+    if (lib) {
+        a = sinf(x[i]);
+        b = cosf(x[i]);
+    } else {
+        fmgi_sincosf(x[i], &a, &b);
+    }
     s[i] = a;
     c[i] = b;
+}
+
+/* ---- per-scene constants: photonmap.cl's OpenCL builtins as ROCm builds them for gfx950 ---------- */
+
+/* length() (opencl.bc _Z6lengthDv3_f): llvm.sqrt with !fpmath 3.0, i.e. v_sqrt_f32 (within 1 ulp, not
+   correctly rounded), of dot(v, v), rescaled below 2^-126 and at inf */
+__device__ float cl_length(f3 a) {
+    const float d = dot3(a, a);
+    if (d < 0x1p-126f) {
+        const f3 t = mul3(a, 0x1p+86f);
+        return __builtin_amdgcn_sqrtf(dot3(t, t)) * 0x1p-86f;
+    }
+    if (d == INFINITY) {
+        const f3 t = mul3(a, 0x1p-66f);
+        return __builtin_amdgcn_sqrtf(dot3(t, t)) * 0x1p+66f;
+    }
+    return __builtin_amdgcn_sqrtf(d);
+}
+
+/* __ocml_rsqrt_f32 with f32 denormals preserved: v_rsq_f32, inputs below 2^-126 scaled by 2^24 */
+__device__ float cl_rsqrt(float x) {
+    const bool tiny = x < 0x1p-126f;
+    const float r = __builtin_amdgcn_rsqf(tiny ? x * 0x1p+24f : x);
+    return tiny ? r * 4096.0f : r;
+}
+
+/* normalize() (opencl.bc _Z9normalizeDv3_f): v * rsqrt(dot(v, v)) with the library's rescaling */
+__device__ f3 cl_normalize(f3 a) {
+    if (a.x == 0.0f && a.y == 0.0f && a.z == 0.0f) return a;
+    float d = dot3(a, a);
+    f3 t = a;
+    if (d < 0x1p-126f) {
+        t = mul3(a, 0x1p+86f);
+        d = dot3(t, t);
+    } else if (d == INFINITY) {
+        t = mul3(a, 0x1p-66f);
+        d = dot3(t, t);
+        if (d == INFINITY) {
+            t = mkf3(copysignf(isinf(t.x) ? 1.0f : 0.0f, t.x), copysignf(isinf(t.y) ? 1.0f : 0.0f, t.y),
+                     copysignf(isinf(t.z) ? 1.0f : 0.0f, t.z));
+            d = dot3(t, t);
+        }
+    }
+    return mul3(t, cl_rsqrt(d));
+}
+
+/* photonmap.cl:43-48 (== :65-70): the sampler basis of a normal */
+__device__ void cl_sampler_basis(f3 n, f3 &bu, f3 &bv) {
+    f3 udir = mkf3(0, 0, 1);
+    if (fabsf(dot3(udir, n)) >= 0.999999f) udir = mkf3(0, 1, 0);
+    const f3 vdir = cl_normalize(cross3(udir, n));
+    bu = cl_normalize(cross3(vdir, n));
+    bv = vdir;
+}
+
+__device__ __forceinline__ f3 f3of(const fmgi_vec3 &v) { return mkf3(v.s[0], v.s[1], v.s[2]); }
+
+/* The per-rect values photonmap.cl recomputes in every intersects() / getTileIdAt() call, and every
+   emitter's and wall's sampler basis, evaluated once per scene with the kernel's own builtins: wl =
+   length(width) (photonmap.cl:144), wn = width / wl (:145), hl, hn (:149-150), bu, bv (:43-48, :65-70).
+   One thread per wall, then one per emitter; the other RectDev / SrcDev fields come from the host. */
+__global__ void k_scene_setup(const fmgi_rect *__restrict__ walls, int nw, const fmgi_rect *__restrict__ srcs, int ns,
+                              RectDev *__restrict__ rd, SrcDev *__restrict__ sd) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    f3 bu, bv;
+    if (i < nw) {
+        const fmgi_rect &r = walls[i];
+        const f3 w = f3of(r.width), h = f3of(r.height);
+        const float wl = cl_length(w), hl = cl_length(h);
+        const f3 wn = div3(w, wl), hn = div3(h, hl);
+        RectDev &d = rd[i];
+        d.wnx = wn.x; d.wny = wn.y; d.wnz = wn.z; d.wl = wl;
+        d.hnx = hn.x; d.hny = hn.y; d.hnz = hn.z; d.hl = hl;
+        d.iwl = 1.0f / wl; /* tile_uv's quotient estimate (checked against a band, fmgi_core.h) */
+        d.ihl = 1.0f / hl;
+        cl_sampler_basis(f3of(r.n), bu, bv);
+        d.bux = bu.x; d.buy = bu.y; d.buz = bu.z;
+        d.bvx = bv.x; d.bvy = bv.y; d.bvz = bv.z;
+    } else if (i - nw < ns) {
+        cl_sampler_basis(f3of(srcs[i - nw].n), bu, bv);
+        SrcDev &d = sd[i - nw];
+        d.bux = bu.x; d.buy = bu.y; d.buz = bu.z;
+        d.bvx = bv.x; d.bvy = bv.y; d.bvz = bv.z;
+    }
 }
 
 /* the bake's arithmetic helpers, one element per thread (fmgi_device_unit) */
@@ -1047,10 +1135,17 @@ hipError_t fmgi_launch_unit(int op, const float *a, const float *b, int32_t *out
     return hipGetLastError();
 }
 
-hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, const FmgiSinCosCoef *coef,
-                              hipStream_t s) {
+hipError_t fmgi_launch_sincos(const float *x, float *sn, float *cs, int64_t n, int lib, hipStream_t s) {
     if (n <= 0) return hipSuccess;
     int64_t blocks = (n + 255) / 256;
-    hipLaunchKernelGGL(k_sincos, dim3((unsigned)blocks), dim3(256), 0, s, x, sn, cs, n, coef);
+    hipLaunchKernelGGL(k_sincos, dim3((unsigned)blocks), dim3(256), 0, s, x, sn, cs, n, lib);
+    return hipGetLastError();
+}
+
+hipError_t fmgi_launch_scene_setup(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, int ns, RectDev *rd,
+                                   SrcDev *sd, hipStream_t s) {
+    const int n = nw + ns;
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_scene_setup, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, walls, nw, srcs, ns, rd, sd);
     return hipGetLastError();
 }

@@ -204,11 +204,14 @@ class Context:
         return {"J": [int(x) for x in sz[:3]], "planes": planes[: 2 * npairs], "cells": cells, "recs": recs,
                 "idx": idx}
 
-    def device_sincosf(self, x: np.ndarray):
+    def device_sincosf(self, x: np.ndarray, library: bool = False):
+        """The samplers' sin/cos on the device (the restatement), or with library=True the device
+        library's sinf/cosf that it restates."""
         x = np.ascontiguousarray(x, np.float32)
         s = np.empty_like(x)
         c = np.empty_like(x)
-        check(self.lib.fmgi_device_sincosf(self.h, _ptr(x), _ptr(s), _ptr(c), len(x)), "fmgi_device_sincosf")
+        fn = self.lib.fmgi_device_sincosf_library if library else self.lib.fmgi_device_sincosf
+        check(fn(self.h, _ptr(x), _ptr(s), _ptr(c), len(x)), "fmgi_device_sincosf")
         return s, c
 
     def device_unit(self, op: int, a: np.ndarray, b: np.ndarray | None = None) -> np.ndarray:

@@ -34,6 +34,7 @@ EXPORTS = (
     "fmgi_trace_items",
     "fmgi_host_sincosf",
     "fmgi_device_sincosf",
+    "fmgi_device_sincosf_library",
     "fmgi_device_unit",
     "fmgi_grid_sizes",
     "fmgi_grid_copy",
@@ -177,6 +178,7 @@ def load() -> C.CDLL:
         "fmgi_trace_items": (C.c_int, [vp, u64, u64, C.c_int, vp, vp, vp]),
         "fmgi_host_sincosf": (None, [vp, vp, vp, i64]),
         "fmgi_device_sincosf": (C.c_int, [vp, vp, vp, vp, i64]),
+        "fmgi_device_sincosf_library": (C.c_int, [vp, vp, vp, vp, i64]),
         "fmgi_device_unit": (C.c_int, [vp, C.c_int, vp, vp, vp, i64]),
         "fmgi_grid_sizes": (C.c_int, [vp, vp]),
         "fmgi_get_stage_cycles": (C.c_int, [vp, vp]),

@@ -261,6 +261,9 @@ int fmgi_grid_copy(const fmgi_context *ctx, void *planes, void *cells, float *re
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);
 /* Device-side twin of fmgi_host_sincosf over n inputs (synchronous; for parity tests). */
 int fmgi_device_sincosf(fmgi_context *ctx, const float *x, float *s, float *c, int64_t n);
+/* The device library's own sinf/cosf (ROCm ocml, what photonmap.cl's sin/cos run on MI355X) over n
+   inputs, for checking the restatement (synchronous; parity tests). */
+int fmgi_device_sincosf_library(fmgi_context *ctx, const float *x, float *s, float *c, int64_t n);
 /* Device arithmetic helpers of the bake kernel over n inputs (synchronous; for parity tests):
    op FMGI_UNIT_SQRT: out[i] = bits of the sampler's correctly rounded sqrtf(a[i]) (b unused);
    op FMGI_UNIT_TRUNC_DIV: out[i] = (int)(a[i] / b[i]), the tile index step of photonmap.cl:108-109

@@ -10,6 +10,7 @@
 
 #include <math.h>
 #include <stdlib.h>
+#include <stdio.h>
 #include <string.h>
 #ifdef _OPENMP
 #include <omp.h>
@@ -23,13 +24,88 @@ static inline v3 vadd(v3 a, v3 b) { return mk(a.x + b.x, a.y + b.y, a.z + b.z); 
 static inline v3 vsub(v3 a, v3 b) { return mk(a.x - b.x, a.y - b.y, a.z - b.z); }
 static inline v3 vmul(v3 a, float s) { return mk(a.x * s, a.y * s, a.z * s); }
 static inline v3 vdiv(v3 a, float s) { return mk(a.x / s, a.y / s, a.z / s); }
-/* OpenCL builtins as fixed by the oracle contract */
-static inline float dot3(v3 a, v3 b) { float t = a.x * b.x; t = t + a.y * b.y; return t + a.z * b.z; }
-static inline v3 cross3(v3 a, v3 b) {
-    return mk(a.y * b.z - a.z * b.y, a.z * b.x - a.x * b.z, a.x * b.y - a.y * b.x);
+/*
+ * OpenCL builtins as ROCm's device libraries implement them for gfx950 -- what the reference kernel
+ * executes on MI355X (opencl.bc / ocml.bc; every llvm.fmuladd there is an FMA on gfx950):
+ *   dot(a, b)   = fma(a.z, b.z, fma(a.y, b.y, a.x * b.x))                         (_Z3dotDv3_fS_)
+ *   cross(a, b) = (fma(a.y, b.z, -(a.z b.y)), fma(a.z, b.x, -(a.x b.z)), fma(a.x, b.y, -(a.y b.x)))
+ *   length(v)   = v_sqrt_f32(dot(v, v)) (llvm.sqrt with !fpmath 3.0), rescaled below 2^-126 / at inf
+ *   normalize(v)= v * v_rsq_f32(dot(v, v)) (__ocml_rsqrt_f32), rescaled likewise; v if v == 0
+ * v_sqrt_f32 and v_rsq_f32 are within 1 ulp, not correctly rounded: hw_sqrt / hw_rsq reproduce them from
+ * truth tables recorded on the MI355X (fmo_set_hw_tables; tests/golden/gfx950_sqrt_rsq.npz).
+ */
+static const int8_t *g_dsqrt, *g_drsq;
+
+void fmo_set_hw_tables(const int8_t *dsqrt, const int8_t *drsq) {
+    g_dsqrt = dsqrt;
+    g_drsq = drsq;
 }
-static inline float len3(v3 a) { return sqrtf(dot3(a, a)); }
-static inline v3 normalize3(v3 a) { return vdiv(a, len3(a)); }
+
+/* base + the recorded ulp delta of x's (exponent parity, mantissa) class; x a positive normal float */
+static float hw_adjust(float base, float x, const int8_t *tab) {
+    if (!tab) {
+        fprintf(stderr, "fm_oracle: gfx950 sqrt/rsq tables not loaded (fmo_set_hw_tables)\n");
+        abort();
+    }
+    uint32_t u, b;
+    memcpy(&u, &x, 4);
+    memcpy(&b, &base, 4);
+    const uint32_t idx = ((((u >> 23) & 0xFFu) - 127u) & 1u) << 23 | (u & 0x7FFFFFu);
+    b = (uint32_t)((int32_t)b + tab[idx]);
+    memcpy(&base, &b, 4);
+    return base;
+}
+
+static float hw_sqrt(float x) { /* v_sqrt_f32 */
+    if (x == 0.0f || !(x < INFINITY)) return sqrtf(x);
+    return hw_adjust((float)sqrt((double)x), x, g_dsqrt);
+}
+
+static float hw_rsq(float x) { /* v_rsq_f32 on a positive normal float */
+    return hw_adjust((float)(1.0 / sqrt((double)x)), x, g_drsq);
+}
+
+static inline float dot3(v3 a, v3 b) { return fmaf(a.z, b.z, fmaf(a.y, b.y, a.x * b.x)); }
+static inline v3 cross3(v3 a, v3 b) {
+    return mk(fmaf(a.y, b.z, -(a.z * b.y)), fmaf(a.z, b.x, -(a.x * b.z)), fmaf(a.x, b.y, -(a.y * b.x)));
+}
+static float len3(v3 a) {
+    const float d = dot3(a, a);
+    if (d < 0x1p-126f) {
+        const v3 s = vmul(a, 0x1p+86f);
+        return hw_sqrt(dot3(s, s)) * 0x1p-86f;
+    }
+    if (d == INFINITY) {
+        const v3 s = vmul(a, 0x1p-66f);
+        return hw_sqrt(dot3(s, s)) * 0x1p+66f;
+    }
+    return hw_sqrt(d);
+}
+static float ocml_rsqrt(float x) { /* __ocml_rsqrt_f32 with f32 denormals preserved (gfx950 OpenCL) */
+    if (x < 0x1p-126f) return x == 0.0f ? INFINITY : hw_rsq(x * 0x1p+24f) * 4096.0f;
+    if (!(x < INFINITY)) return 0.0f;
+    return hw_rsq(x);
+}
+static v3 normalize3(v3 a) {
+    if (a.x == 0.0f && a.y == 0.0f && a.z == 0.0f) return a;
+    float d = dot3(a, a);
+    v3 s = a;
+    if (d < 0x1p-126f) {
+        s = vmul(a, 0x1p+86f);
+        d = dot3(s, s);
+    } else if (d == INFINITY) {
+        s = vmul(a, 0x1p-66f);
+        d = dot3(s, s);
+        if (d == INFINITY) {
+            s = mk(copysignf(isinf(s.x) ? 1.0f : 0.0f, s.x), copysignf(isinf(s.y) ? 1.0f : 0.0f, s.y),
+                   copysignf(isinf(s.z) ? 1.0f : 0.0f, s.z));
+            d = dot3(s, s);
+        }
+    }
+    return vmul(s, ocml_rsqrt(d));
+}
+/* the reference HOST's length() (vector3_cl.c:93: sqrtf(x*x + y*y + z*z), gcc without FMA) */
+static float host_len3(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
 
 /* photonmap.cl:21-25 -- LCG, returns (float)s / (float)0xFFFFFFFF == (float)s * 2^-32 */
 float fmo_rand(uint32_t *s) {
@@ -37,9 +113,32 @@ float fmo_rand(uint32_t *s) {
     return (float)(*s) / 4294967296.0f;
 }
 
+/* sin/cos as ROCm's device library computes them on gfx9+ (ocml.bc __ocml_sin_f32 / __ocml_cos_f32,
+   the fast-FMA path) for 0 <= x < 2^17: k = rint(x * 2/pi), a three-part Cody-Waite reduction with FMAs,
+   minimax polynomials; quadrant k & 3. Checked bit for bit against the device library on every
+   reachable phi (tests/test_gpu_parity.py). */
 void fmo_sincos(float x, float *s, float *c) {
-    *s = (float)sin((double)x);
-    *c = (float)cos((double)x);
+    float k = rintf(x * 0x1.45f306p-1f);
+    float r = fmaf(k, -0x1.921fb4p+0f, x);
+    r = fmaf(k, -0x1.4442d0p-24f, r);
+    r = fmaf(k, -0x1.846988p-48f, r);
+    int q = (int)k & 3;
+    float z = r * r;
+    float p = fmaf(z, -0x1.983304p-13f, 0x1.110388p-7f);
+    p = fmaf(z, p, -0x1.55553ap-3f);
+    p = z * p;
+    float sn = fmaf(r, p, r);
+    float cp = fmaf(z, 0x1.aea668p-16f, -0x1.6c9e76p-10f);
+    cp = fmaf(z, cp, 0x1.5557eep-5f);
+    cp = fmaf(z, cp, -0x1.000008p-1f);
+    float cs = fmaf(z, cp, 1.0f);
+    float so = (q & 1) ? cs : sn, co = (q & 1) ? -sn : cs;
+    *s = q > 1 ? -so : so;
+    *c = q > 1 ? -co : co;
+}
+
+void fmo_sincos_n(const float *x, float *s, float *c, int64_t n) {
+    for (int64_t i = 0; i < n; i++) fmo_sincos(x[i], &s[i], &c[i]);
 }
 
 /* photonmap.cl:27-52 (sky, fold=1) and :54-74 (cosine, fold=0) */
@@ -195,7 +294,7 @@ static void work_item(uint32_t rng, const fmo_rect *win, const fmo_rect *rects, 
 
 /* global_illumination_cl.c:217-222: per-source work-item count */
 static uint64_t source_items(const fmo_rect *src, float spa, uint64_t wg) {
-    float area = len3(ld(src->width)) * len3(ld(src->height));
+    float area = host_len3(ld(src->width)) * host_len3(ld(src->height));
     uint64_t n = (uint64_t)((spa * area) / 100);
     return (n / wg + 1) * wg;
 }

@@ -6,13 +6,18 @@
  * and bench.py's cpu_baseline leg may load it, and only as the checker / CPU baseline.
  * The product path (libflatmatch_gi.so) never links, loads or calls anything in oracle/.
  *
- * Arithmetic contract (the "oracle semantics"):
- *   - IEEE-754 binary32 for every float op of photonmap.cl, evaluated exactly in source
- *     order, no FMA contraction (-ffp-contract=off), correctly rounded div and sqrt;
- *   - OpenCL builtins: dot(a,b) = (a.x*b.x + a.y*b.y) + a.z*b.z, cross = textbook form,
- *     length = sqrt(dot(a,a)), normalize(a) = a / length(a);
- *   - sin/cos of the float argument = (float)sin((double)x) / (float)cos((double)x);
+ * Arithmetic contract (the "oracle semantics"): photonmap.cl as ROCm's
+ * OpenCL compiler builds it for gfx950 with IEEE division/sqrt and no contraction (the reference
+ * kernel on MI355X, oracle/build_ref.sh "strict"):
+ *   - IEEE-754 binary32 for every float op written in photonmap.cl, in source order, no FMA
+ *     contraction, correctly rounded `/` and sqrt();
+ *   - the OpenCL builtins as ROCm's device libraries define them: dot and cross as FMA chains,
+ *     length(v) = v_sqrt_f32(dot(v,v)), normalize(v) = v * v_rsq_f32(dot(v,v)) (the hardware ops
+ *     are reproduced from truth tables recorded on the MI355X, fmo_set_hw_tables), sin/cos = the
+ *     device library's fp32 algorithm (OCML __ocml_sin_f32 / __ocml_cos_f32);
  *   - `pos.s2 > 0.0005` compares in double (the literal is a double, photonmap.cl:236);
+ *   - host-side code (the launch schedule's area, global_illumination_cl.c:217) keeps the host's
+ *     own length() (vector3_cl.c:93);
  *   - texel accumulation is the race-free sum: each deposit channel (always a multiple of
  *     2^-25) is added EXACTLY into an int64 fixed-point accumulator.
  *
@@ -91,6 +96,10 @@ void fmo_trace_item_f32(const fmo_rect *rects, int nrects, const fmo_rect *sourc
 /* The reference's float RNG and sampler pieces, exposed for unit tests. */
 float fmo_rand(uint32_t *state);
 void fmo_sincos(float x, float *s, float *c);
+void fmo_sincos_n(const float *x, float *s, float *c, int64_t n);
+/* gfx950 v_sqrt_f32 / v_rsq_f32 truth tables: int8 ulp deltas from the once-rounded double value for
+   x in [1, 4) (index = exponent parity << 23 | mantissa); must be set before any trace. */
+void fmo_set_hw_tables(const int8_t *dsqrt, const int8_t *drsq);
 
 /* Convert the fixed-point sums to float texels the way the product does:
    out = (float)((double)in + (double)sum * 2^-25). texels4 has 4 floats per texel. */

@@ -30,6 +30,22 @@ class OracleStats(C.Structure):
 
 
 _lib = None
+_hw_tables = None
+HW_TABLES = os.path.join(os.path.dirname(HERE), "tests", "golden", "gfx950_sqrt_rsq.npz")
+
+
+def hw_tables():
+    """gfx950's v_sqrt_f32 / v_rsq_f32 as int8 ulp deltas [2^24] each (recorded on the MI355X by
+    tools/hw_sqrt_rsq_table.hip; packed 2 bits per entry in tests/golden/gfx950_sqrt_rsq.npz)."""
+    d = np.load(HW_TABLES)
+    out = []
+    for k in ("sqrt", "rsq"):
+        p = d[k]
+        v = np.empty(4 * len(p), np.int8)
+        for j in range(4):
+            v[j::4] = ((p >> (2 * j)) & 3).astype(np.int8) - 1
+        out.append(np.ascontiguousarray(v))
+    return out
 
 
 def build():
@@ -65,6 +81,13 @@ def load():
         lib.rad_oracle.argtypes = [vp, C.c_int, vp, C.c_int, vp, C.c_int, C.c_int, vp, vp, C.c_int]
         lib.ao_oracle_tree.restype = i64
         lib.ao_oracle_tree.argtypes = [vp, C.c_int, vp, i64]
+        lib.fmo_sincos_n.restype = None
+        lib.fmo_sincos_n.argtypes = [vp, vp, vp, i64]
+        lib.fmo_set_hw_tables.restype = None
+        lib.fmo_set_hw_tables.argtypes = [vp, vp]
+        global _hw_tables
+        _hw_tables = hw_tables()
+        lib.fmo_set_hw_tables(_p(_hw_tables[0]), _p(_hw_tables[1]))
         _lib = lib
     return _lib
 
@@ -154,6 +177,26 @@ def finalize(lm_fx: np.ndarray, texels_in: np.ndarray) -> np.ndarray:
     out = np.empty_like(tin)
     lib.fmo_finalize(_p(lm), len(tin), _p(tin), _p(out))
     return out
+
+
+def sincos(x: np.ndarray):
+    """The oracle's sin/cos of the samplers (ROCm device-library algorithm) over an array."""
+    lib = load()
+    x = np.ascontiguousarray(x, np.float32)
+    s, c = np.empty_like(x), np.empty_like(x)
+    lib.fmo_sincos_n(_p(x), _p(s), _p(c), len(x))
+    return s, c
+
+
+def reachable_phi() -> np.ndarray:
+    """Every phi = 6.283184f * rand() the samplers can draw (photonmap.cl:33,57; rand() = (float)s * 2^-32
+    for a u32 s, photonmap.cl:21-25): 83,886,081 values, in increasing order."""
+    parts = [np.arange(0, 2**24, dtype=np.float64)]
+    for e in range(24, 32):
+        parts.append(np.arange(2.0**e, 2.0 ** (e + 1), 2.0 ** (e - 23)))
+    parts.append(np.array([2.0**32]))
+    f = np.concatenate(parts).astype(np.float32)
+    return np.float32(6.283184) * (f * np.float32(2.0**-32))
 
 
 def rand_sequence(state: int, n: int) -> np.ndarray:

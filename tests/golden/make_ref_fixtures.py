@@ -53,11 +53,23 @@ def main():
     offs = np.load(os.path.join(HERE, "glibc_rand_4096.npy"))
     out_dir = sys.argv[1] if len(sys.argv) > 1 else HERE
     summary = {}
-    cases = [
-        ("example", S.load_geometry(os.path.join(HERE, "example_geometry.bin"), "example"), 65_000,
-         [(0, range(0, 96)), (7, range(0, 32))]),
+    example = S.load_geometry(os.path.join(HERE, "example_geometry.bin"), "example")
+    apartment = S.load_geometry(os.path.join(HERE, "apartment30_geometry.bin"), "apartment30")
+    cases = [  # (fixture name, scene, spa, [(launch index, gids)])
+        ("example", example, 65_000, [(0, range(0, 96)), (7, range(0, 32))]),
         ("box200", S.box_scene(200), 172_413_793, [(0, range(1000, 1048))]),
+        # BASELINE config 2 schedule (43 launches): late launches, rng offsets deep in the glibc prefix
+        ("example_late", example, 6_500_000, [(40, range(0, 32)), (42, range(10_400, 10_432))]),
+        # BASELINE config 4 schedule (3,907 launches): the last two launches
+        ("box200_late", S.box_scene(200), 1_724_137_931, [(3905, range(0, 32)), (3906, range(6_600, 6_632))]),
+        # BASELINE config 5 (2000 rects): the first and the last launch
+        ("box2000", S.box_scene(2000), 172_413_793, [(0, range(1000, 1032)), (390, range(16_000, 16_032))]),
+        # generated 30-room layout (654 walls, 34 sources): a window launch and the last light launch
+        ("apartment30", apartment, 3_000_000, [(0, range(0, 32)), (77, range(19_900, 19_932))]),
     ]
+    only = os.environ.get("FMGI_REF_CASES")  # e.g. "box2000,apartment30": regenerate a subset
+    if only:
+        cases = [c for c in cases if c[0] in only.split(",")]
     for name, sc, spa, parts in cases:
         L = O.schedule_with_offsets(sc, spa, offs)
         for variant in ("strict", "relaxed"):
@@ -76,7 +88,12 @@ def main():
             summary[f"{name}/{variant}"] = {"items": n_tot, "bit_identical_to_oracle": n_same,
                                             "max_rel_item_total_diff": worst}
     print(json.dumps(summary, indent=1))
-    with open(os.path.join(out_dir, "ref_items_summary.json"), "w") as f:
+    path = os.path.join(out_dir, "ref_items_summary.json")
+    if only and os.path.exists(path):  # keep the entries of the cases not regenerated
+        old = json.load(open(path))
+        old.update(summary)
+        summary = old
+    with open(path, "w") as f:
         json.dump(summary, f, indent=1)
 
 

@@ -1,0 +1,176 @@
+"""GPU parity at the BASELINE configurations' full sizes (global_illumination_cl.c:215-272 schedules).
+
+  config 2  example.png, spa 6,500,000: 100,121,600 photons in 43 launches -- the whole int64 lightmap
+            against the oracle, bit for bit (the oracle needs ~20 s on the GPU box's 16 cores)
+  config 4  box200, spa 1,724,137,931: 10,000,025,600 photons in 3,907 launches on one GPU (several
+            memory-sized stream chunks) -- size-independent properties (chunk and split invariance,
+            photon / scan / deposit accounting, no stream overflow) plus an exact oracle window taken
+            from the schedule's LAST launches, whose rng offsets lie deep in the glibc prefix
+  config 5  box2000: a 1e7-photon prefix against the oracle for every scan and accumulation mode
+  apartment30 (654 walls, 34 sources; the grid's per-axis walk with binary search and records-box
+            skip): per-photon traces and a lightmap prefix against the oracle
+"""
+import os
+
+import numpy as np
+import pytest
+
+import fm_oracle as O
+import fmgi
+from conftest import GOLDEN
+
+pytestmark = pytest.mark.gpu
+
+KERNELS = [fmgi.KERNEL_EXACT, fmgi.KERNEL_FAST, fmgi.KERNEL_GRID]
+
+
+@pytest.fixture(scope="module")
+def offsets():
+    return np.load(os.path.join(GOLDEN, "glibc_rand_4096.npy"))
+
+
+@pytest.fixture(scope="module")
+def apartment30():
+    from fmgi import scene
+
+    return scene.load_geometry(os.path.join(GOLDEN, "apartment30_geometry.bin"), "apartment30")
+
+
+def _ctx(sc, spa, offsets, accum=fmgi.ACCUM_AUTO):
+    ctx = fmgi.Context(0)
+    ctx.set_accumulation(accum)
+    ctx.set_scene(sc)
+    ctx.plan(spa, rng_offsets=offsets)
+    return ctx
+
+
+def _bake_gpu(torch, ctx, b, e, kernel=fmgi.KERNEL_AUTO):
+    s = torch.cuda.Stream()
+    with torch.cuda.stream(s):
+        lm = torch.zeros((ctx.scene.num_texels, 4), dtype=torch.int64, device="cuda")
+        ctx.bake_items(b, e, lm.data_ptr(), kernel, s.cuda_stream)
+    s.synchronize()
+    return lm.cpu().numpy()
+
+
+def _compare_traces(sc, ctx, L, b, e, kernel):
+    ev, cnt, rngf = ctx.trace_items(b, e, kernel)
+    for w in range(b, e):
+        li = int(np.searchsorted(L["item_begin"], w, side="right") - 1)
+        gid = w - int(L[li]["item_begin"])
+        state = (gid + int(L[li]["rng_offset"])) & 0xFFFFFFFF
+        oev, ofin = O.trace_item(sc, int(L[li]["source"]), int(L[li]["is_window"]), state)
+        k = w - b
+        assert cnt[k] == len(oev), f"item {w}: {cnt[k]} vs {len(oev)} bounces"
+        g = ev[k, : cnt[k]]
+        assert np.array_equal(g.view(np.uint32), oev.view(np.uint32).reshape(g.view(np.uint32).shape)), f"item {w}"
+        assert rngf[k] == ofin, f"item {w}: final RNG"
+
+
+def test_config2_full_lightmap_exact(torch_cuda, example_scene, offsets):
+    """BASELINE config 2 at full size: every one of the 100,121,600 photons, bit-exact."""
+    spa = 6_500_000
+    L = O.schedule_with_offsets(example_scene, spa, offsets)
+    assert len(L) == 43
+    ctx = _ctx(example_scene, spa, offsets)
+    assert ctx.get_plan().tobytes() == L.tobytes()
+    n = ctx.total_items
+    assert 100 * n == 100_121_600
+    ctx.reset_stats()
+    lm = _bake_gpu(torch_cuda, ctx, 0, n)
+    st = ctx.stats()
+    olm, ost = O.bake(example_scene, L)
+    assert np.array_equal(lm[:, :3], olm)
+    assert not lm[:, 3].any()
+    for k in ("photons", "scans", "deposits", "escapes"):
+        assert st[k] == ost[k], k
+    assert st["stream_overflow"] == 0
+    ctx.close()
+
+
+def test_config4_full_size_properties_and_late_window(torch_cuda, box200, offsets):
+    """BASELINE config 4 on one GPU: 1e10 photons. The oracle cannot trace 1e10 photons, so: the whole
+    bake equals the sum of two halves baked in several forced chunks (exact integer sums are order-free),
+    the counters account for every photon, and the last launches' items equal the oracle exactly."""
+    spa = 1_724_137_931
+    L = O.schedule_with_offsets(box200, spa, offsets)
+    assert len(L) == 3907
+    ctx = _ctx(box200, spa, offsets)
+    assert ctx.get_plan().tobytes() == L.tobytes()
+    n = ctx.total_items
+    assert 100 * n == 10_000_025_600
+    ctx.reset_stats()
+    full = _bake_gpu(torch_cuda, ctx, 0, n)
+    st = ctx.stats()
+    assert st["photons"] == 100 * n
+    assert st["deposits"] + st["escapes"] == st["scans"]
+    assert st["stream_overflow"] == 0
+    assert int(full[:, :3].astype(np.float64).sum()) >= st["deposits"] * 3 * (2**25 // 4)
+    os.environ["FMGI_CHUNK_ITEMS"] = "17000000"  # ~3 chunks per half through one buffer set
+    try:
+        h1 = _bake_gpu(torch_cuda, ctx, 0, n // 2)
+        h2 = _bake_gpu(torch_cuda, ctx, n // 2, n)
+    finally:
+        os.environ.pop("FMGI_CHUNK_ITEMS", None)
+    assert np.array_equal(full, h1 + h2)
+    assert ctx.stats()["stream_overflow"] == 0
+    # exact window: the last 4,096 items (launches 3905-3906), lightmap and per-photon traces
+    b = n - 4096
+    assert int(L[3905]["item_begin"]) < b
+    win = _bake_gpu(torch_cuda, ctx, b, n)
+    olm, _ = O.bake(box200, L, b, n)
+    assert np.array_equal(win[:, :3], olm)
+    _compare_traces(box200, ctx, L, n - 64, n, fmgi.KERNEL_GRID)
+    ctx.close()
+
+
+@pytest.fixture(scope="module")
+def box2000_prefix(box2000, offsets):
+    """box2000 (BASELINE config 5) items [5,000, 105,000): 1e7 photons through the oracle, once."""
+    spa = 172_413_793
+    L = O.schedule_with_offsets(box2000, spa, offsets)
+    b, e = 5_000, 105_000
+    olm, ost = O.bake(box2000, L, b, e)
+    return spa, b, e, olm, ost
+
+
+@pytest.mark.parametrize("kernel,accum", [(fmgi.KERNEL_GRID, fmgi.ACCUM_STREAM), (fmgi.KERNEL_GRID, fmgi.ACCUM_FX3),
+                                          (fmgi.KERNEL_GRID, fmgi.ACCUM_STATE), (fmgi.KERNEL_FAST, fmgi.ACCUM_STREAM),
+                                          (fmgi.KERNEL_EXACT, fmgi.ACCUM_STREAM)])
+def test_box2000_1e7_photons_exact(torch_cuda, box2000, offsets, box2000_prefix, kernel, accum):
+    spa, b, e, olm, ost = box2000_prefix
+    ctx = _ctx(box2000, spa, offsets, accum)
+    ctx.reset_stats()
+    lm = _bake_gpu(torch_cuda, ctx, b, e, kernel)
+    st = ctx.stats()
+    assert np.array_equal(lm[:, :3], olm)
+    for k in ("photons", "scans", "deposits", "escapes"):
+        assert st[k] == ost[k], k
+    if kernel == fmgi.KERNEL_GRID:  # the near-tie fallback of the grid scan is exercised at this size
+        assert st["exact_rescans"] > 1000
+    ctx.close()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_apartment30_traces(torch_cuda, apartment30, offsets, kernel):
+    spa = 3_000_000
+    L = O.schedule_with_offsets(apartment30, spa, offsets)
+    ctx = _ctx(apartment30, spa, offsets)
+    assert ctx.get_plan().tobytes() == L.tobytes()
+    _compare_traces(apartment30, ctx, L, 0, 128, kernel)  # window 0
+    last = int(L[-1]["item_begin"])
+    _compare_traces(apartment30, ctx, L, last, last + 64, kernel)  # the last light
+    ctx.close()
+
+
+@pytest.mark.parametrize("kernel", KERNELS)
+def test_apartment30_lightmap_prefix_exact(torch_cuda, apartment30, offsets, kernel):
+    spa = 3_000_000
+    L = O.schedule_with_offsets(apartment30, spa, offsets)
+    ctx = _ctx(apartment30, spa, offsets)
+    n = ctx.total_items
+    for b, e in ((0, 20_000), (n - 20_000, n)):
+        lm = _bake_gpu(torch_cuda, ctx, b, e, kernel)
+        olm, _ = O.bake(apartment30, L, b, e)
+        assert np.array_equal(lm[:, :3], olm), (b, e)
+    ctx.close()

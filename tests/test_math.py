@@ -1,36 +1,50 @@
-"""The sampler's sin/cos (csrc/fmgi_math.h) against glibc on every reachable input.
+"""The samplers' sin/cos (csrc/fmgi_math.h) on every reachable input, and the roulette threshold.
 
-photonmap.cl:33,57 draw phi = 6.283184f * rand() with rand() = (float)s * 2^-32 (photonmap.cl:21-25),
-so phi takes ~8.4e7 distinct values. The parity contract fixes sin/cos to (float)sin((double)phi); the
-exhaustive C checker (tests/tools/check_sincos.c) verifies fmgi_sincosf reproduces glibc bit for bit
-on all of them. The GPU twin of this test is in test_gpu_parity.py."""
+photonmap.cl:33,57 draw phi = 6.283184f * rand() with rand() = (float)s * 2^-32 (photonmap.cl:21-25), so
+phi takes 83,886,081 distinct values. On the MI355X the reference's sin/cos come from ROCm's device
+library (ocml.bc __ocml_sin_f32 / __ocml_cos_f32, fp32, not correctly rounded); the product and the
+oracle restate that algorithm independently. Here (CPU): product restatement == oracle restatement on
+every reachable phi, and both equal the device library's own results as recorded on the MI355X
+(tests/golden/ocml_sincos.json: SHA-256 of all 2 x 83,886,081 result bits). The GPU twin
+(test_gpu_parity.py) checks the device restatement against the device library directly."""
+import hashlib
+import json
 import os
-import subprocess
 
 import numpy as np
 
+import fm_oracle as O
 import fmgi
-from conftest import PKG, REPO
+from conftest import GOLDEN
 
 
-def test_sincos_exhaustive_vs_glibc(tmp_path):
-    exe = tmp_path / "check_sincos"
-    subprocess.run(
-        ["g++", "-x", "c++", "-O2", "-ffp-contract=off", "-fopenmp", "-I", os.path.join(PKG, "csrc"),
-         os.path.join(REPO, "tests", "tools", "check_sincos.c"), "-o", str(exe), "-lm"],
-        check=True,
-    )
-    out = subprocess.run([str(exe)], capture_output=True, text=True, check=True, timeout=600).stdout.split()
-    checked, bad = int(out[-2]), int(out[-1])
-    assert checked == 83_886_081
-    assert bad == 0
+def _digest(s, c):
+    return hashlib.sha256(s.view(np.uint32).tobytes() + c.view(np.uint32).tobytes()).hexdigest()
 
 
-def test_library_sincos_matches_numpy_double_rounding():
-    xs = np.float32(6.283184) * (np.arange(0, 2**32, 2**20 + 12345, dtype=np.uint64).astype(np.float32) * np.float32(2.0**-32))
-    s, c = fmgi.host_sincosf(xs)
-    assert np.array_equal(s, np.sin(xs.astype(np.float64)).astype(np.float32))
-    assert np.array_equal(c, np.cos(xs.astype(np.float64)).astype(np.float32))
+def test_sincos_restatements_agree_on_every_reachable_phi_and_match_the_device_library():
+    phi = O.reachable_phi()
+    assert len(phi) == 83_886_081
+    hs, hc = fmgi.host_sincosf(phi)
+    os_, oc = O.sincos(phi)
+    assert np.array_equal(hs.view(np.uint32), os_.view(np.uint32))
+    assert np.array_equal(hc.view(np.uint32), oc.view(np.uint32))
+    golden = json.load(open(os.path.join(GOLDEN, "ocml_sincos.json")))
+    assert golden["inputs"] == len(phi)
+    assert _digest(hs, hc) == golden["sha256_sin_cos_bits"]
+
+
+def test_device_library_sincos_is_not_correctly_rounded():
+    """Why the contract names the library: its fp32 sin/cos differ from the correctly rounded values
+    (float)sin((double)phi) on a sizeable share of inputs (~17 % of the reachable phi, mostly by 1 ulp)."""
+    phi = O.reachable_phi()[::97]
+    s, c = fmgi.host_sincosf(phi)
+    es = np.sin(phi.astype(np.float64)).astype(np.float32)
+    ec = np.cos(phi.astype(np.float64)).astype(np.float32)
+    differ = (s != es) | (c != ec)
+    assert 0.05 < differ.mean() < 0.4
+    ulps = np.abs(s.view(np.int32).astype(np.int64) - es.view(np.int32).astype(np.int64))
+    assert ulps.max() <= 4
 
 
 def test_roulette_threshold_is_the_double_comparison():

@@ -1,10 +1,13 @@
 """The oracle pinned against the REFERENCE KERNEL's own output (CPU test over committed fixtures).
 
-tests/golden/ref_items_<scene>_<variant>.npz were produced on an MI355X by make_ref_fixtures.py: the
+tests/golden/ref_items_<case>_<variant>.npz were produced on an MI355X by make_ref_fixtures.py: the
 reference photonmap.cl, compiled for gfx950 with ROCm's OpenCL device libraries (oracle/build_ref.sh),
 launched one work item per launch on a zeroed lightColors buffer. Here the oracle's fp32 per-item sum
 (fm_oracle.trace_item_f32: the same deposits added in the same order) must reproduce those lightmaps:
-  strict  (IEEE div/sqrt, no contraction = the oracle contract): every item bit for bit;
+  strict  (IEEE div/sqrt, no contraction = the oracle contract, with the OpenCL builtins as ROCm builds
+          them for gfx950): every item bit for bit -- 432 items over example.png (configs 1 and 2, incl.
+          the config-2 schedule's last launches), box200 (config 3 and the last launches of config 4),
+          box2000 (config 5) and the generated 30-room layout;
   relaxed (-cl-unsafe-math-optimizations): the same deposit totals, most items bit for bit -- relaxed
           math moves a few hit points across texel boundaries, it does not change colours.
 """
@@ -27,13 +30,25 @@ def _items(path):
                    d[f"texel_{p}"][b[k] : b[k + 1]], d[f"value_{p}"][b[k] : b[k + 1]])
 
 
-def _scene(name, example_scene, box200):
-    return {"example": example_scene, "box200": box200}[name]
+def _scene(name, example_scene, box200, box2000):
+    from fmgi import scene
+
+    if name == "apartment30":
+        return scene.load_geometry(os.path.join(GOLDEN, "apartment30_geometry.bin"), "apartment30")
+    return {"example": example_scene, "example_late": example_scene, "box200": box200, "box200_late": box200,
+            "box2000": box2000}[name]
 
 
-@pytest.mark.parametrize("name,n_items", [("example", 128), ("box200", 48)])
-def test_oracle_reproduces_reference_kernel_strict(name, n_items, example_scene, box200):
-    sc = _scene(name, example_scene, box200)
+# (fixture, items): launches 0/7 of config 1 and item 1000.. of config 3 (round 1); late launches of the
+# config-2 and config-4 schedules (rng offsets deep in the glibc prefix), the first and last launch of
+# config 5 (box2000) and the generated 30-room layout (round 2)
+PINNED = [("example", 128), ("box200", 48), ("example_late", 64), ("box200_late", 64), ("box2000", 64),
+          ("apartment30", 64)]
+
+
+@pytest.mark.parametrize("name,n_items", PINNED)
+def test_oracle_reproduces_reference_kernel_strict(name, n_items, example_scene, box200, box2000):
+    sc = _scene(name, example_scene, box200, box2000)
     seen = 0
     for src, isw, st, tex, val in _items(os.path.join(GOLDEN, f"ref_items_{name}_strict.npz")):
         mine = O.trace_item_f32(sc, src, isw, st)
@@ -44,9 +59,10 @@ def test_oracle_reproduces_reference_kernel_strict(name, n_items, example_scene,
     assert seen == n_items
 
 
-@pytest.mark.parametrize("name,min_identical", [("example", 120), ("box200", 42)])
-def test_relaxed_math_reference_stays_close(name, min_identical, example_scene, box200):
-    sc = _scene(name, example_scene, box200)
+@pytest.mark.parametrize("name,min_identical", [("example", 120), ("box200", 42), ("example_late", 56),
+                                                 ("box200_late", 56), ("box2000", 56), ("apartment30", 56)])
+def test_relaxed_math_reference_stays_close(name, min_identical, example_scene, box200, box2000):
+    sc = _scene(name, example_scene, box200, box2000)
     same = total = 0
     for src, isw, st, tex, val in _items(os.path.join(GOLDEN, f"ref_items_{name}_relaxed.npz")):
         mine = O.trace_item_f32(sc, src, isw, st)
