@@ -101,7 +101,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
                                                    unsigned long long *__restrict__ lm, int num_texels) {
     /* per texel of the tile: sum R, sum (G - R), sum (B - R) (int64 modulo 2^64; the true sums of G and
        B are non-negative), so a grey code costs one LDS add and a tinted one three */
-    extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [4096] + colours */
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
     unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
     const int t = blockIdx.x / G, g = blockIdx.x % G;
@@ -156,13 +156,8 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
     hipLaunchKernelGGL(k_slice_sort, dim3((unsigned)nslices), dim3(256), 0, s, sb.stream, sb.cursor, sb.cap, P,
                        sb.sorted, sb.toff);
     const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 64 KiB: two workgroups per CU */
-    static bool lds_set = false;
-    if (!lds_set) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_tile_runs, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           (int)lds);
-        if (e != hipSuccess) return e;
-        lds_set = true;
-    }
+    hipError_t e = fmgi_set_lds_attr_once<0>((const void *)k_tile_runs, (int)lds);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * sb.groups)), dim3(sb.block > 0 ? sb.block : 1024), lds, s, sb.sorted, sb.toff,
                        sb.cursor, sb.cap, P, sb.groups, (const uint4 *)sb.colpack, lm, num_texels);
     return hipGetLastError();

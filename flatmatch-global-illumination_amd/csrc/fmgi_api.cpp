@@ -23,6 +23,7 @@
 #include <algorithm>
 #include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/flatmatch_gi.h"
@@ -413,6 +414,7 @@ struct fmgi_context {
     uint32_t launch_cap = 0;
     uint64_t *d_src_item_begin = nullptr; /* [nsrc + 1] */
     int32_t *d_src_launch0 = nullptr;     /* [nsrc]     */
+    int64_t d_src_cap = 0;
     unsigned long long *d_counter = nullptr;
     unsigned long long *d_stats = nullptr;
     /* ScanFast filter image + non-axis-aligned rect list */
@@ -651,6 +653,33 @@ FMGI_API int fmgi_set_accumulation(fmgi_context *c, int mode) {
 
 FMGI_API int fmgi_get_accumulation(fmgi_context *c) { return c ? c->accum : set_err(FMGI_ERR_ARG, "null context"); }
 
+/* workgroup size of the bake (FMGI_BLOCK: experiments, 64..1024 lanes) */
+static int bake_block() {
+    int block = 256;
+    if (const char *be = getenv("FMGI_BLOCK"))
+        if (atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) block = atoi(be);
+    return block;
+}
+
+/* dynamic LDS a bake launch may use without raising the kernel's limit: the scan image staged in LDS
+   (FAST: 64 B per record pair, GRID: 128 B per plane pair) plus the per-wave code rings must fit, or the
+   launch fails; a scene whose image does not fit runs a kernel whose image does, or the exact scan (no
+   image, identical results) */
+static const size_t kBakeLdsLimit = 65536;
+
+static bool kernel_fits(const fmgi_context *c, int kernel, int accum, int block) {
+    if (kernel == FMGI_KERNEL_EXACT) return true;
+    const int img = kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : c->fimg_bytes;
+    return fmgi_bake_lds(kernel, accum, block, img, nullptr) <= kBakeLdsLimit;
+}
+
+static int fitting_kernel(const fmgi_context *c, int kernel, int accum, int block) {
+    if (kernel_fits(c, kernel, accum, block)) return kernel;
+    const int other = kernel == FMGI_KERNEL_GRID ? FMGI_KERNEL_FAST : FMGI_KERNEL_GRID;
+    if (kernel != FMGI_KERNEL_EXACT && kernel_fits(c, other, accum, block)) return other;
+    return FMGI_KERNEL_EXACT;
+}
+
 FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
                             int num_windows, const fmgi_rect *lights, int num_lights, int num_texels) {
     if (!c || num_walls < 0 || num_windows < 0 || num_lights < 0 || num_texels < 0 ||
@@ -684,6 +713,8 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
         c->auto_kernel = (4 * slots < pairs) ? FMGI_KERNEL_GRID : FMGI_KERNEL_FAST;
+        /* the largest LDS use (STREAM rings) decides, so the choice holds for every accumulation mode */
+        c->auto_kernel = fitting_kernel(c, c->auto_kernel, FMGI_ACCUM_STREAM, bake_block());
     }
     if (c->device != FMGI_HOST_ONLY) {
     HIPCHK(hipSetDevice(c->device));
@@ -813,13 +844,17 @@ FMGI_API int64_t fmgi_plan(fmgi_context *c, int spa, int wg, const int32_t *rng_
         sib[(size_t)L[k].source] = L[k].item_begin;
         sl0[(size_t)L[k].source] = (int32_t)k;
     }
-    hipFree(c->d_src_item_begin);
-    hipFree(c->d_src_launch0);
-    c->d_src_item_begin = nullptr;
-    c->d_src_launch0 = nullptr;
-    HIPCHK(hipMalloc(&c->d_src_item_begin, sib.size() * sizeof(uint64_t)));
+    if ((int64_t)sib.size() > c->d_src_cap) { /* grown only: repeated plans of one scene allocate nothing */
+        hipFree(c->d_src_item_begin);
+        hipFree(c->d_src_launch0);
+        c->d_src_item_begin = nullptr;
+        c->d_src_launch0 = nullptr;
+        c->d_src_cap = 0;
+        HIPCHK(hipMalloc(&c->d_src_item_begin, sib.size() * sizeof(uint64_t)));
+        HIPCHK(hipMalloc(&c->d_src_launch0, sib.size() * sizeof(int32_t)));
+        c->d_src_cap = (int64_t)sib.size();
+    }
     HIPCHK(hipMemcpy(c->d_src_item_begin, sib.data(), sib.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
-    HIPCHK(hipMalloc(&c->d_src_launch0, sl0.size() * sizeof(int32_t)));
     HIPCHK(hipMemcpy(c->d_src_launch0, sl0.data(), sl0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     }
     c->launch_cap = (uint32_t)cap;
@@ -901,6 +936,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
                                                   (unsigned long long)c->total_items);
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_AUTO) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     if (kernel == FMGI_KERNEL_AUTO) kernel = c->auto_kernel;
+    const int block = bake_block();
+    kernel = fitting_kernel(c, kernel, c->accum, block); /* an image too large for LDS: same results, other scan */
     if (b == e) return FMGI_OK;
     if (c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     /* no walls: every photon escapes at its first scan (photonmap.cl:208), so nothing is deposited */
@@ -944,9 +981,6 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.ev_counts = counts;
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
-    int block = 256;
-    if (const char *be = getenv("FMGI_BLOCK")) /* experiments: 64..1024 lanes per workgroup */
-        if (atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) block = atoi(be);
     fmgi_bake_lds(kernel, c->accum, block, a.fimg_bytes, &a.ring_off);
     if (c->accum != FMGI_ACCUM_STREAM) {
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
@@ -1218,19 +1252,31 @@ FMGI_API int fmgi_device_unit(fmgi_context *c, int op, const float *a, const flo
  * the caller sees exactly those calls). The HIP runtime's first device initialisation in a process
  * draws from the same generator (observed on ROCm 7: one call inside the first hipStreamCreate /
  * allocation). So the schedule is built, with its rand() calls, before any HIP call, and the state is
- * snapshotted then and restored after the device work. glibc keeps the TYPE_3 state in a 128-byte
- * array whose first word records the read position; setstate() re-reads it from there.
+ * snapshotted then and restored after the device work. glibc keeps the state of random_r's TYPE_n
+ * generator in the caller's array: a header word (MAX_TYPES * rear + type, just the type for TYPE_0)
+ * followed by the degree-n table; setstate() re-reads everything from there. The guard saves and
+ * restores exactly that many bytes for the type the header names.
  */
 struct RandGuard {
     char *state = nullptr;
-    char saved[128];
+    size_t bytes = 0;
+    char saved[4 * 64];
     bool ok = false;
     void save() {
 #ifdef __GLIBC__
         static char scratch[128];
         state = initstate(1, scratch, sizeof scratch); /* records the position in state[0], switches away */
         if (!state) return;
-        memcpy(saved, state, sizeof saved);
+        int32_t hdr;
+        memcpy(&hdr, state, 4);
+        static const int kDegree[5] = {0, 7, 15, 31, 63}; /* TYPE_0 .. TYPE_4 (glibc random_r.c) */
+        const int type = hdr % 5;
+        if (hdr < 0 || type < 0 || type > 4) { /* not a header glibc wrote: leave the state alone */
+            setstate(state);
+            return;
+        }
+        bytes = (size_t)4 * (std::max(kDegree[type], 1) + 1); /* header + table (TYPE_0: one LCG word) */
+        memcpy(saved, state, bytes);
         setstate(state); /* back to the caller's array and position */
         ok = true;
 #endif
@@ -1240,20 +1286,129 @@ struct RandGuard {
         if (!ok) return;
         static char scratch2[128];
         initstate(1, scratch2, sizeof scratch2); /* leave the caller's array (its header is rewritten) */
-        memcpy(state, saved, sizeof saved);
+        memcpy(state, saved, bytes);
         setstate(state);
 #endif
     }
 };
 
 /*
- * One bake of a reference Geometry on all GPUs of the node (FMGI_GPUS, default: every visible device,
- * at most 8). The reference launch schedule is built once (libc rand() consumed exactly as the
- * reference does, global_illumination_cl.c:251) and its flattened work items are split into equal
- * contiguous shards, one per GPU; each GPU accumulates its own exact int64 lightmap, and the shards are
- * summed on GPU 0 over xGMI peer copies (integer sums: the result is bit-identical for any GPU count).
- * FMGI_SHARDS (tests only) splits into more shards than GPUs, round-robin, to exercise the reduction on
- * a single device.
+ * The drop-in's device state, cached across calls: per shard a context (scene tables, launch schedule,
+ * stream buffers) and its lightmap buffers, keyed by a hash of the geometry, so a repeated call on the
+ * same scene uploads nothing but the schedule and the caller's texels (the reference rebuilds its
+ * OpenCL context on every call, global_illumination_cl.c:279-286; nothing here requires that).
+ * fmgi_dropin_release() frees it; FMGI_DROPIN_CACHE=0 frees it after every call.
+ */
+struct DropinShard {
+    fmgi_context *ctx = nullptr;
+    uint64_t scene_hash = 0;
+    void *lm = nullptr;    /* int64 [numTexels][4] */
+    void *stage = nullptr; /* a peer shard's lightmap during the reduction */
+    size_t lm_bytes = 0, stage_bytes = 0;
+    hipEvent_t done = nullptr;
+};
+static std::mutex g_dropin_mu;
+static std::vector<DropinShard> g_dropin;
+static void *g_dropin_tex = nullptr;
+static size_t g_dropin_tex_bytes = 0;
+static int g_dropin_tex_dev = -1;
+static bool g_peer_on[64][64];
+
+static void dropin_release_shard(DropinShard &S) {
+    if (S.ctx && hipSetDevice(S.ctx->device) == hipSuccess) {
+        (void)hipStreamSynchronize(S.ctx->stream);
+        (void)hipFree(S.lm);
+        (void)hipFree(S.stage);
+        if (S.done) (void)hipEventDestroy(S.done);
+    }
+    fmgi_destroy(S.ctx);
+    S = DropinShard{};
+}
+
+static void dropin_release_locked() {
+    for (DropinShard &S : g_dropin) dropin_release_shard(S);
+    g_dropin.clear();
+    if (g_dropin_tex && hipSetDevice(g_dropin_tex_dev) == hipSuccess) (void)hipFree(g_dropin_tex);
+    g_dropin_tex = nullptr;
+    g_dropin_tex_bytes = 0;
+    g_dropin_tex_dev = -1;
+}
+
+FMGI_API void fmgi_dropin_release(void) {
+    std::lock_guard<std::mutex> lk(g_dropin_mu);
+    dropin_release_locked();
+}
+
+/* FNV-1a over the geometry the bake reads (walls, windows, lights, numTexels) */
+static uint64_t geometry_hash(const fmgi_geometry *geo) {
+    uint64_t h = 1469598103934665603ull;
+    auto mix = [&](const void *p, size_t n) {
+        const unsigned char *b = (const unsigned char *)p;
+        for (size_t i = 0; i < n; i++) h = (h ^ b[i]) * 1099511628211ull;
+    };
+    const int32_t counts[4] = {geo->numWalls, geo->numWindows, geo->numLights, geo->numTexels};
+    mix(counts, sizeof counts);
+    if (geo->numWalls > 0) mix(geo->walls, sizeof(fmgi_rect) * (size_t)geo->numWalls);
+    if (geo->numWindows > 0) mix(geo->windows, sizeof(fmgi_rect) * (size_t)geo->numWindows);
+    if (geo->numLights > 0) mix(geo->lights, sizeof(fmgi_rect) * (size_t)geo->numLights);
+    return h | 1; /* 0 = "no scene" */
+}
+
+/* peer access dev -> peer (xGMI), once per pair; false if the pair cannot (copies then stage as HIP does) */
+static void enable_peer(int dev, int peer) {
+    if (dev == peer || dev >= 64 || peer >= 64 || g_peer_on[dev][peer]) return;
+    int can = 0;
+    if (hipDeviceCanAccessPeer(&can, dev, peer) == hipSuccess && can && hipSetDevice(dev) == hipSuccess) {
+        const hipError_t e = hipDeviceEnablePeerAccess(peer, 0);
+        if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) g_peer_on[dev][peer] = true;
+        (void)hipGetLastError(); /* an "already enabled" must not linger as the thread's last error */
+    }
+}
+
+/* the stream-accumulation overflow flag of a context's bakes since its reset (never set by sizing; a set
+   flag means dropped deposits, so the call fails instead of returning a wrong lightmap) */
+static int check_no_overflow(fmgi_context *c) {
+    unsigned long long v = 0;
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipMemcpy(&v, c->d_stats + KSTAT_OVERFLOW, sizeof v, hipMemcpyDeviceToHost));
+    if (v) return set_err(FMGI_ERR_STATE, "stream accumulation overflowed (%llu blocks dropped)", v);
+    return FMGI_OK;
+}
+
+/* The drop-in's shard layout: shard k runs on device k % ngpu over the contiguous work items
+   [items * k / nshard, items * (k + 1) / nshard). */
+FMGI_API int fmgi_dropin_shards(uint64_t items, int ngpu, int nshard, int32_t *dev, uint64_t *begin, uint64_t *end) {
+    if (ngpu < 1 || nshard < 1 || !dev || !begin || !end) return set_err(FMGI_ERR_ARG, "fmgi_dropin_shards: bad arguments");
+    for (int k = 0; k < nshard; k++) {
+        dev[k] = k % ngpu;
+        begin[k] = items * (uint64_t)k / (uint64_t)nshard;
+        end[k] = items * (uint64_t)(k + 1) / (uint64_t)nshard;
+    }
+    return FMGI_OK;
+}
+
+/* ... and its reduction: a binary tree into shard 0; step i adds shard src[i] into shard dst[i], and the
+   steps of one round (distance d) are independent. Returns the number of steps (nshard - 1). */
+FMGI_API int fmgi_dropin_reduce_order(int nshard, int32_t *dst, int32_t *src) {
+    if (nshard < 1 || (nshard > 1 && (!dst || !src))) return set_err(FMGI_ERR_ARG, "fmgi_dropin_reduce_order: bad arguments");
+    int n = 0;
+    for (int d = 1; d < nshard; d *= 2)
+        for (int k = 0; k + d < nshard; k += 2 * d) {
+            dst[n] = k;
+            src[n] = k + d;
+            n++;
+        }
+    return n;
+}
+
+/*
+ * One bake of a reference Geometry, sharded over FMGI_GPUS devices of the node (default 1, the
+ * reference's one device; at most 8). The reference launch schedule is built once (libc rand() consumed
+ * exactly as the reference does, global_illumination_cl.c:251) and its flattened work items are split
+ * into equal contiguous shards, one per GPU, prepared and launched concurrently (a host thread per
+ * shard); each GPU accumulates its own exact int64 lightmap, and the shards are summed in a binary tree
+ * over xGMI peer copies into shard 0 (integer sums: bit-identical for any GPU count). FMGI_SHARDS (tests)
+ * splits into more shards than GPUs, round-robin, to exercise the reduction on a single device.
  */
 static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int kernel,
                                  const std::vector<int32_t> &offs, uint64_t items, fmgi_vec3 *texels_out,
@@ -1286,7 +1441,13 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     }
     RandGuard guard;
     guard.save();
-    const int rc_all = bake_geometry_devices(geo, spa, wg, kernel, offs, items, texels_out, verbose);
+    int rc_all;
+    {
+        std::lock_guard<std::mutex> lk(g_dropin_mu);
+        rc_all = bake_geometry_devices(geo, spa, wg, kernel, offs, items, texels_out, verbose);
+        const char *ce = getenv("FMGI_DROPIN_CACHE");
+        if (rc_all != FMGI_OK || (ce && atoi(ce) == 0)) dropin_release_locked();
+    }
     guard.restore();
     return rc_all;
 }
@@ -1296,82 +1457,140 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
     int ndev = fmgi_device_count();
     if (ndev <= 0) return set_err(FMGI_ERR_NO_DEVICE, "no HIP device visible");
     const char *g_env = getenv("FMGI_GPUS");
-    int ngpu = g_env ? atoi(g_env) : std::min(ndev, 8);
-    ngpu = std::max(1, std::min(ngpu, ndev));
+    int ngpu = g_env ? atoi(g_env) : 1;
+    ngpu = std::max(1, std::min(std::min(ngpu, ndev), 8));
     const char *s_env = getenv("FMGI_SHARDS");
-    int nshard = s_env ? std::max(1, std::min(atoi(s_env), 64)) : ngpu;
+    const int nshard = s_env ? std::max(1, std::min(atoi(s_env), 64)) : ngpu;
+    const uint64_t hash = geometry_hash(geo);
+    const size_t tb = (size_t)geo->numTexels * 16, lmb = 2 * tb; /* float4 texels, int64 x 4 lightmap */
+    if ((int)g_dropin.size() > nshard) { /* fewer shards than the cached call: drop the extra ones */
+        for (size_t k = (size_t)nshard; k < g_dropin.size(); k++) dropin_release_shard(g_dropin[k]);
+        g_dropin.resize((size_t)nshard);
+    }
+    g_dropin.resize((size_t)nshard);
 
-    std::vector<fmgi_context *> ctx((size_t)nshard, nullptr);
-    std::vector<void *> lm((size_t)nshard, nullptr);
-    void *d_tex = nullptr, *d_stage = nullptr;
-    size_t tb = (size_t)geo->numTexels * 16;
-    int rc = FMGI_OK;
-    for (int k = 0; k < nshard && rc == FMGI_OK; k++) {
-        ctx[k] = fmgi_create(k % ngpu);
-        if (!ctx[k]) { rc = FMGI_ERR_HIP; break; }
-        rc = fmgi_set_scene(ctx[k], geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
-                            geo->numLights, geo->numTexels);
-        if (rc != FMGI_OK) break;
+    std::vector<int32_t> sdev((size_t)nshard);
+    std::vector<uint64_t> sbeg((size_t)nshard), send((size_t)nshard);
+    fmgi_dropin_shards(items, ngpu, nshard, sdev.data(), sbeg.data(), send.data());
+    /* per shard: context (cached), scene (if changed), schedule, lightmap buffers, bake launch */
+    auto prepare_and_launch = [&](int k, std::string &err) -> int {
+        DropinShard &S = g_dropin[(size_t)k];
+        const int dev = sdev[(size_t)k];
+        if (S.ctx && S.ctx->device != dev) dropin_release_shard(S);
+        if (!S.ctx) {
+            S.ctx = fmgi_create(dev);
+            if (!S.ctx) { err = fmgi_last_error(); return FMGI_ERR_HIP; }
+        }
+        fmgi_context *c = S.ctx;
+        int rc = FMGI_OK;
+        if (S.scene_hash != hash) {
+            S.scene_hash = 0;
+            rc = fmgi_set_scene(c, geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
+                                geo->numLights, geo->numTexels);
+            if (rc != FMGI_OK) { err = fmgi_last_error(); return rc; }
+            S.scene_hash = hash;
+        }
         /* every shard replays the schedule planned above (the rand() values in offs) */
-        const int64_t nl = fmgi_plan(ctx[k], spa, wg, offs.data(), (int64_t)offs.size(), nullptr);
-        if (nl < 0) rc = (int)nl;
-        else if (k == 0 && verbose) {
-            hipDeviceProp_t prop;
-            if (hipGetDeviceProperties(&prop, 0) != hipSuccess) prop.name[0] = 0;
-            printf("[INF] Selected device '%s' (x%d)\n\n", prop.name, ngpu);
-            printf("photon-mapping %d light sources with %llu M samples in %lld reference launches\n",
-                   ctx[0]->nsrcs, (unsigned long long)(items * 100 / 1000000), (long long)nl);
-            fflush(stdout);
+        const int64_t nl = fmgi_plan(c, spa, wg, offs.data(), (int64_t)offs.size(), nullptr);
+        if (nl < 0) { err = fmgi_last_error(); return (int)nl; }
+        if (geo->numTexels <= 0) return FMGI_OK;
+        hipError_t e = hipSetDevice(dev);
+        if (e == hipSuccess && S.lm_bytes < lmb) {
+            (void)hipFree(S.lm);
+            S.lm = nullptr;
+            S.lm_bytes = 0;
+            e = hipMalloc(&S.lm, lmb);
+            if (e == hipSuccess) S.lm_bytes = lmb;
+        }
+        if (e == hipSuccess && nshard > 1 && S.stage_bytes < lmb) {
+            (void)hipFree(S.stage);
+            S.stage = nullptr;
+            S.stage_bytes = 0;
+            e = hipMalloc(&S.stage, lmb);
+            if (e == hipSuccess) S.stage_bytes = lmb;
+        }
+        if (e == hipSuccess && !S.done) e = hipEventCreateWithFlags(&S.done, hipEventDisableTiming);
+        if (e == hipSuccess) e = hipMemsetAsync(S.lm, 0, lmb, c->stream);
+        if (e == hipSuccess) e = hipMemsetAsync(c->d_stats + KSTAT_OVERFLOW, 0, sizeof(unsigned long long), c->stream);
+        if (e != hipSuccess) {
+            err = std::string("shard buffers on device ") + std::to_string(dev) + ": " + hipGetErrorString(e);
+            return FMGI_ERR_OOM;
+        }
+        rc = fmgi_bake_items(c, sbeg[(size_t)k], send[(size_t)k], S.lm, kernel, c->stream);
+        if (rc == FMGI_OK && hipEventRecord(S.done, c->stream) != hipSuccess) rc = set_err(FMGI_ERR_HIP, "event");
+        if (rc != FMGI_OK) err = fmgi_last_error();
+        return rc;
+    };
+    std::vector<int> rcs((size_t)nshard, FMGI_OK);
+    std::vector<std::string> errs((size_t)nshard);
+    if (nshard == 1) {
+        rcs[0] = prepare_and_launch(0, errs[0]);
+    } else { /* shards set up and launch concurrently, one host thread each */
+        std::vector<std::thread> th;
+        for (int k = 0; k < nshard; k++) th.emplace_back([&, k] { rcs[(size_t)k] = prepare_and_launch(k, errs[(size_t)k]); });
+        for (std::thread &t : th) t.join();
+    }
+    for (int k = 0; k < nshard; k++)
+        if (rcs[(size_t)k] != FMGI_OK) return set_err(rcs[(size_t)k], "shard %d: %s", k, errs[(size_t)k].c_str());
+    DropinShard &S0 = g_dropin[0];
+    if (verbose) {
+        hipDeviceProp_t prop;
+        if (hipGetDeviceProperties(&prop, S0.ctx->device) != hipSuccess) prop.name[0] = 0;
+        printf("[INF] Selected device '%s' (x%d)\n\n", prop.name, ngpu);
+        printf("photon-mapping %d light sources with %llu M samples in %lld reference launches\n", S0.ctx->nsrcs,
+               (unsigned long long)(items * 100 / 1000000), (long long)S0.ctx->h_launches.size());
+        fflush(stdout);
+    }
+    if (geo->numTexels <= 0) return FMGI_OK;
+    /* binary-tree reduction into shard 0 (fmgi_dropin_reduce_order), ordered by events across devices */
+    std::vector<int32_t> rdst((size_t)nshard), rsrc((size_t)nshard);
+    const int nsteps = fmgi_dropin_reduce_order(nshard, rdst.data(), rsrc.data());
+    {
+        for (int i = 0; i < nsteps; i++) {
+            DropinShard &D = g_dropin[(size_t)rdst[(size_t)i]], &Src = g_dropin[(size_t)rsrc[(size_t)i]];
+            const int dd = D.ctx->device, sd = Src.ctx->device;
+            enable_peer(dd, sd);
+            hipError_t e = hipSetDevice(dd);
+            if (e == hipSuccess) e = hipStreamWaitEvent(D.ctx->stream, Src.done, 0);
+            const void *add_src = Src.lm;
+            if (e == hipSuccess && dd != sd) { /* over xGMI into this device's staging buffer */
+                e = hipMemcpyPeerAsync(D.stage, dd, Src.lm, sd, lmb, D.ctx->stream);
+                add_src = D.stage;
+            }
+            if (e == hipSuccess)
+                e = fmgi_launch_add_u64((unsigned long long *)D.lm, (const unsigned long long *)add_src,
+                                        (int64_t)geo->numTexels * 4, D.ctx->stream);
+            if (e == hipSuccess) e = hipEventRecord(D.done, D.ctx->stream);
+            if (e != hipSuccess) return set_err(FMGI_ERR_HIP, "shard reduction: %s", hipGetErrorString(e));
         }
     }
-    if (rc == FMGI_OK && geo->numTexels > 0) {
-        /* launch every shard before waiting on any (all devices bake concurrently) */
-        for (int k = 0; k < nshard && rc == FMGI_OK; k++) {
-            fmgi_context *c = ctx[k];
-            if (hipSetDevice(c->device) != hipSuccess || hipMalloc(&lm[k], tb * 2) != hipSuccess) {
-                rc = set_err(FMGI_ERR_OOM, "lightmap buffer (%zu B) on device %d", tb * 2, c->device);
-                break;
-            }
-            if (hipMemsetAsync(lm[k], 0, tb * 2, c->stream) != hipSuccess) rc = set_err(FMGI_ERR_HIP, "memset");
-            uint64_t b = items * (uint64_t)k / (uint64_t)nshard, e = items * (uint64_t)(k + 1) / (uint64_t)nshard;
-            if (rc == FMGI_OK) rc = fmgi_bake_items(c, b, e, lm[k], kernel, c->stream);
-        }
-        fmgi_context *c0 = ctx[0];
-        if (rc == FMGI_OK) {
-            hipError_t e = hipSetDevice(c0->device);
-            if (e == hipSuccess) e = hipMalloc(&d_tex, tb);
-            if (e == hipSuccess) e = hipMemcpyAsync(d_tex, geo->texels, tb, hipMemcpyHostToDevice, c0->stream);
-            if (e == hipSuccess && nshard > 1) e = hipMalloc(&d_stage, tb * 2);
-            for (int k = 1; k < nshard && e == hipSuccess; k++) { /* sum shard k into shard 0 on GPU 0 */
-                e = hipStreamSynchronize(ctx[k]->stream);
-                if (e == hipSuccess)
-                    e = hipMemcpyPeerAsync(d_stage, c0->device, lm[k], ctx[k]->device, tb * 2, c0->stream);
-                if (e == hipSuccess)
-                    e = fmgi_launch_add_u64((unsigned long long *)lm[0], (const unsigned long long *)d_stage,
-                                            (int64_t)geo->numTexels * 4, c0->stream);
-            }
-            if (e != hipSuccess) rc = set_err(FMGI_ERR_HIP, "shard reduction: %s", hipGetErrorString(e));
-        }
-        if (rc == FMGI_OK) rc = fmgi_finalize(c0, lm[0], d_tex, d_tex, c0->stream);
-        if (rc == FMGI_OK) {
-            hipError_t e = hipMemcpyAsync(texels_out, d_tex, tb, hipMemcpyDeviceToHost, c0->stream);
-            if (e == hipSuccess) e = hipStreamSynchronize(c0->stream);
-            if (e != hipSuccess) rc = set_err(FMGI_ERR_HIP, "bake: %s", hipGetErrorString(e));
-        }
+    /* texels: the caller's values + the exact sum, rounded once (k_finalize), on shard 0's device */
+    fmgi_context *c0 = S0.ctx;
+    HIPCHK(hipSetDevice(c0->device));
+    if (g_dropin_tex && (g_dropin_tex_dev != c0->device || g_dropin_tex_bytes < tb)) {
+        int cur = 0;
+        (void)hipGetDevice(&cur);
+        (void)hipSetDevice(g_dropin_tex_dev);
+        (void)hipFree(g_dropin_tex);
+        (void)hipSetDevice(cur);
+        g_dropin_tex = nullptr;
+        g_dropin_tex_bytes = 0;
     }
+    if (!g_dropin_tex) {
+        HIPCHK(hipMalloc(&g_dropin_tex, tb));
+        g_dropin_tex_bytes = tb;
+        g_dropin_tex_dev = c0->device;
+    }
+    HIPCHK(hipMemcpyAsync(g_dropin_tex, geo->texels, tb, hipMemcpyHostToDevice, c0->stream));
+    int rc = fmgi_finalize(c0, S0.lm, g_dropin_tex, g_dropin_tex, c0->stream);
+    if (rc != FMGI_OK) return rc;
+    HIPCHK(hipMemcpyAsync(texels_out, g_dropin_tex, tb, hipMemcpyDeviceToHost, c0->stream));
+    HIPCHK(hipStreamSynchronize(c0->stream));
     for (int k = 0; k < nshard; k++) {
-        if (!ctx[k]) continue;
-        if (hipSetDevice(ctx[k]->device) == hipSuccess) {
-            (void)hipStreamSynchronize(ctx[k]->stream);
-            (void)hipFree(lm[k]);
-            if (k == 0) {
-                (void)hipFree(d_tex);
-                (void)hipFree(d_stage);
-            }
-        }
-        fmgi_destroy(ctx[k]);
+        rc = check_no_overflow(g_dropin[(size_t)k].ctx);
+        if (rc != FMGI_OK) return rc;
     }
-    return rc;
+    return FMGI_OK;
 }
 
 FMGI_API int getGlobalIlluminationCl(const fmgi_geometry *geo, int numSamplesPerArea, fmgi_vec3 *texels_out) {

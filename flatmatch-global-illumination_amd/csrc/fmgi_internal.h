@@ -8,6 +8,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include "fmgi_lds_attr.h"
+
 #include "fmgi_core.h"
 
 /* One axis-aligned rectangle as the conservative filter sees it (32 B = one s_load_dwordx8):

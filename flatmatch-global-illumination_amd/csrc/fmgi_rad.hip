@@ -10,6 +10,7 @@
  */
 #include <hip/hip_runtime.h>
 
+#include "fmgi_lds_attr.h"
 #include "fmgi_rad.h"
 
 #pragma clang fp contract(off)
@@ -285,13 +286,8 @@ hipError_t fmgi_rad_launch_rays(const RadArgs &a, hipStream_t s) {
     if (a.sort_n < 2 || a.sort_n > FMGI_RAD_MAX_SORT || (a.sort_n & (a.sort_n - 1)) || a.nrects > a.sort_n)
         return hipErrorInvalidValue;
     const size_t lds = (size_t)a.sort_n * 8;
-    static bool attr = false;
-    if (!attr) {
-        hipError_t e = hipFuncSetAttribute((const void *)k_rad_rays, hipFuncAttributeMaxDynamicSharedMemorySize,
-                                           FMGI_RAD_MAX_SORT * 8);
-        if (e != hipSuccess) return e;
-        attr = true;
-    }
+    hipError_t e = fmgi_set_lds_attr_once<1>((const void *)k_rad_rays, FMGI_RAD_MAX_SORT * 8);
+    if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_rad_rays, dim3((unsigned)a.nchunk), dim3(256), lds, s, a);
     return hipGetLastError();
 }

@@ -18,6 +18,8 @@ import ctypes as C
 import numpy as np
 
 from . import scene
+
+HOST_ONLY = -1  # FMGI_HOST_ONLY: a context without a device (scene checks and planning only)
 from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, RadStats, Timing, FmgiError, Geometry, Stats,
                    check, load)
 from .scene import RECT_DTYPE, Scene
@@ -246,6 +248,28 @@ def make_geometry(sc: Scene, texels: np.ndarray):
     g.numTexels = sc.num_texels
     g.texels = texels.ctypes.data
     return g, keep
+
+
+def dropin_release():
+    """Free the device state the drop-in entry points cache across calls (fmgi_dropin_release)."""
+    load().fmgi_dropin_release()
+
+
+def dropin_shards(items: int, ngpu: int, nshard: int):
+    """The drop-in's multi-GPU layout: (device, begin, end) per shard (fmgi_dropin_shards)."""
+    dev = np.zeros(nshard, np.int32)
+    b = np.zeros(nshard, np.uint64)
+    e = np.zeros(nshard, np.uint64)
+    check(load().fmgi_dropin_shards(items, ngpu, nshard, _ptr(dev), _ptr(b), _ptr(e)), "fmgi_dropin_shards")
+    return dev, b, e
+
+
+def dropin_reduce_order(nshard: int):
+    """The drop-in's shard reduction: (dst, src) pairs in execution order (fmgi_dropin_reduce_order)."""
+    dst = np.zeros(max(nshard, 1), np.int32)
+    src = np.zeros(max(nshard, 1), np.int32)
+    n = check(load().fmgi_dropin_reduce_order(nshard, _ptr(dst), _ptr(src)), "fmgi_dropin_reduce_order")
+    return dst[:n], src[:n]
 
 
 def bake_geometry(sc: Scene, spa: int, texels: np.ndarray | None = None) -> np.ndarray:

@@ -16,6 +16,9 @@ LIB_PATH = os.path.join(PKG_DIR, f"libflatmatch_gi_{os.environ['FMGI_LIB']}.so" 
 EXPORTS = (
     "performGlobalIlluminationCl",
     "getGlobalIlluminationCl",
+    "fmgi_dropin_release",
+    "fmgi_dropin_shards",
+    "fmgi_dropin_reduce_order",
     "fmgi_version",
     "fmgi_last_error",
     "fmgi_device_count",
@@ -178,6 +181,9 @@ def load() -> C.CDLL:
         "fmgi_trace_items": (C.c_int, [vp, u64, u64, C.c_int, vp, vp, vp]),
         "fmgi_host_sincosf": (None, [vp, vp, vp, i64]),
         "fmgi_device_sincosf": (C.c_int, [vp, vp, vp, vp, i64]),
+        "fmgi_dropin_shards": (C.c_int, [C.c_uint64, C.c_int, C.c_int, vp, vp, vp]),
+        "fmgi_dropin_reduce_order": (C.c_int, [C.c_int, vp, vp]),
+        "fmgi_dropin_release": (None, []),
         "fmgi_device_sincosf_library": (C.c_int, [vp, vp, vp, vp, i64]),
         "fmgi_device_unit": (C.c_int, [vp, C.c_int, vp, vp, vp, i64]),
         "fmgi_grid_sizes": (C.c_int, [vp, vp]),

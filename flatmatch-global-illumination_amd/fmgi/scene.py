@@ -198,6 +198,26 @@ def box_scene(n_rects: int = 200, room=(10.0, 8.0, 2.6), tile_size: float = TILE
     return Scene(name, walls, window, lights, ntex)
 
 
+def shelves_scene(n_panels: int = 6000, tile_size: float = 4.0, seed: int = 7) -> Scene:
+    """box200 plus n_panels small horizontal panels, each on its own height (half facing up, half
+    down): thousands of distinct planes, so neither scan image (ScanFast's record pairs, ScanGrid's
+    plane pairs) fits in LDS and the bake must fall back to the exact scan (fmgi_api.cpp kernel_fits)."""
+    box = box_scene(200, tile_size=tile_size)
+    rng = np.random.default_rng(seed)
+    walls = list(box.walls)
+    for i in range(n_panels):
+        z = f32(0.2 + 2.2 * (i + 0.5) / n_panels)
+        x, y = f32(rng.uniform(0.5, 9.0)), f32(rng.uniform(0.5, 7.0))
+        w, h = f32(rng.uniform(0.1, 0.5)), f32(rng.uniform(0.1, 0.5))
+        if i % 2:  # normal +z: width along -x from the far corner (parseLayout.c:471 floor convention)
+            walls.append(create_rectangle(f32(x + w), y, z, f32(-w), 0, 0, 0, h, 0, tile_size))
+        else:      # normal -z (ceiling convention)
+            walls.append(create_rectangle(x, y, z, w, 0, 0, 0, h, 0, tile_size))
+    walls = np.array(walls, RECT_DTYPE)
+    ntex = assign_texel_bases(walls)
+    return Scene(f"shelves{n_panels}", walls, box.windows, box.lights, ntex)
+
+
 def spa_for_photons(scene: Scene, photons: float) -> int:
     """numSamplesPerArea giving ~`photons` photons over the scene's emitters (main.c:58 semantics)."""
     area = 0.0

@@ -20,7 +20,7 @@
  * Environment knobs the reference ABI cannot carry (read by performGlobalIlluminationCl):
  *   FMGI_WG        virtual OpenCL work-group size of the launch schedule (default 256, the value
  *                  ROCm's OpenCL reports for CL_KERNEL_WORK_GROUP_SIZE; global_illumination_cl.c:300)
- *   FMGI_GPUS      number of GPUs to shard over (default: all visible, max 8)
+ *   FMGI_GPUS      number of GPUs one drop-in call shards over (default 1, like the reference; max 8)
  *   FMGI_KERNEL    "auto" (default), "grid", "fast" or "exact" -- all produce identical bits; see DESIGN.md
  *   FMGI_QUIET     1 = suppress the reference's progress line
  */
@@ -61,6 +61,13 @@ void performGlobalIlluminationCl(fmgi_geometry *geo, int numSamplesPerArea);
    written to texels_out[numTexels] (initial values taken from geo->texels, which is not modified).
    Returns 0 on success, a negative fmgi error code otherwise (no exit()). */
 int getGlobalIlluminationCl(const fmgi_geometry *geo, int numSamplesPerArea, fmgi_vec3 *texels_out);
+/* The drop-in entry points keep their device state (contexts, scene tables, stream buffers) across
+   calls, keyed by the geometry; this frees it (FMGI_DROPIN_CACHE=0: freed after every call). */
+void fmgi_dropin_release(void);
+/* The drop-in's multi-GPU layout (host only; for tests): shard k -> device dev[k], work items
+   [begin[k], end[k]); and its binary-tree reduction into shard 0 (returns the step count, nshard - 1). */
+int fmgi_dropin_shards(uint64_t items, int ngpu, int nshard, int32_t *dev, uint64_t *begin, uint64_t *end);
+int fmgi_dropin_reduce_order(int nshard, int32_t *dst, int32_t *src);
 
 /* ---- Ambient occlusion ------------------------------------------------------ */
 /* The reference's performAmbientOcclusionNative (global_illumination_native.h:16, photonmap.c:478-490)

@@ -159,3 +159,39 @@ def test_no_gpu_fails_loudly(tmp_path):
     r = subprocess.run(["python", str(prog)], capture_output=True, text=True, env=env, timeout=120)
     assert r.returncode == 255, r.stdout + r.stderr
     assert "[Err] performGlobalIlluminationCl" in r.stdout and "UNREACHABLE" not in r.stdout
+
+
+@pytest.mark.parametrize("items,ngpu,nshard", [(100_000_256, 8, 8), (1_001_216, 4, 4), (17, 2, 3), (5, 8, 8),
+                                                (391 * 25_600, 3, 7), (0, 2, 2)])
+def test_dropin_shard_layout_and_reduction_tree(items, ngpu, nshard):
+    """The drop-in's multi-GPU plan (used by bake_geometry_devices): shards partition the work items in
+    order, land on devices 0..ngpu-1 (device indices > 0 included), and the reduction tree adds every
+    other shard into shard 0 exactly once, each source finished before it is read."""
+    dev, b, e = fmgi.dropin_shards(items, ngpu, nshard)
+    assert list(dev) == [k % ngpu for k in range(nshard)]
+    assert b[0] == 0 and e[-1] == items and np.all(b[1:] == e[:-1]) and np.all(e >= b)
+    assert max(e - b) - min(e - b) <= 1
+    dst, src = fmgi.dropin_reduce_order(nshard)
+    assert len(dst) == nshard - 1
+    total = {k: {k} for k in range(nshard)}
+    consumed = set()
+    for d, s in zip(dst, src):
+        assert d < s and s not in consumed and d not in consumed
+        total[int(d)] |= total.pop(int(s))
+        consumed.add(int(s))
+    assert total == {0: set(range(nshard))}
+
+
+def test_scan_image_too_large_for_lds_falls_back():
+    """A scene with thousands of distinct planes: neither ScanFast's record image nor ScanGrid's plane
+    image fits the 64-KiB dynamic LDS of a bake launch, so AUTO resolves to the exact scan (same
+    results) instead of a launch that would fail; small scenes keep their LDS scans."""
+    from fmgi import scene
+
+    big = scene.shelves_scene(6000)
+    ctx = fmgi.Context(fmgi.HOST_ONLY)
+    ctx.set_scene(big)
+    assert ctx.auto_kernel == fmgi.KERNEL_EXACT
+    ctx.set_scene(scene.box_scene(200))
+    assert ctx.auto_kernel == fmgi.KERNEL_GRID
+    ctx.close()

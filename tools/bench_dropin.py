@@ -1,10 +1,11 @@
 #!/usr/bin/env python
 """End-to-end time of the drop-in boundary (not the BASELINE metric): what the reference's main.c sees
 when it calls performGlobalIlluminationCl (global_illumination_cl.c:275-321) linked against
-libflatmatch_gi.so. Each call creates its device contexts, plans the reference launch schedule
-(consuming libc rand() once per launch), uploads the geometry, bakes, reduces the GPU shards, adds the
-sums to the caller's texels and copies them back -- as the reference re-creates its OpenCL context and
-recompiles photonmap.cl on every call.
+libflatmatch_gi.so. Each call plans the reference launch schedule (consuming libc rand() once per
+launch), bakes, reduces the GPU shards, adds the sums to the caller's texels and copies them back; the
+device contexts, scene tables and buffers are cached across calls per geometry (fmgi_dropin_release;
+--no-cache frees them after every call, as the reference re-creates its OpenCL context and recompiles
+photonmap.cl on every call).
 
   python tools/bench_dropin.py [--reps 3]
 
@@ -33,7 +34,10 @@ CASES = [  # (BASELINE config, scene, numSamplesPerArea)
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--no-cache", action="store_true", help="FMGI_DROPIN_CACHE=0: no device state kept between calls")
     a = ap.parse_args()
+    if a.no_cache:
+        os.environ["FMGI_DROPIN_CACHE"] = "0"
     os.environ.setdefault("FMGI_QUIET", "1")
     import fmgi
     from fmgi import scene
@@ -53,6 +57,7 @@ def main():
             ts.append(time.perf_counter() - t0)
         print(json.dumps({"metric": "drop-in photons/s (wall time of one performGlobalIlluminationCl-equivalent call)",
                           "config": desc, "spa": spa, "photons": photons, "gpus": fmgi.device_count(),
+                          "cache": not a.no_cache,
                           "first_call_s": ts[0], "warm_call_s": min(ts[1:]),
                           "warm_photons_per_s": photons / min(ts[1:]),
                           "texel_sum": float(out[:, :3].astype(np.float64).sum())}), flush=True)

@@ -5,6 +5,8 @@
 #   rad / radprof    tools/bench_rad.py $RAD_ARGS (plain / under rocprofv3 --kernel-trace --stats)
 #   ref              reference-kernel pin (tests/golden/make_ref_fixtures.py)
 #   ocml             the device library's sin/cos digest (tests/golden/make_ocml_fixture.py)
+#   valu             VALU issue ceilings (tools/valu_peak)
+#   dropin           drop-in boundary timing, cached and uncached (tools/bench_dropin.py)
 #   bench            python bench.py $BENCH_ARGS
 #   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
 #   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
@@ -33,6 +35,8 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     radprof) step radprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/radprof" -o run --output-format csv -- python tools/bench_rad.py --reps 1 --no-cpu-baseline ${RAD_ARGS:-} ;;
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;
     ocml)  step ocml 300 python tests/golden/make_ocml_fixture.py "$OUT" ;;
+    valu)  step valu 120 ./tools/valu_peak ;;
+    dropin) step dropin 600 python tools/bench_dropin.py && step dropin_nocache 600 python tools/bench_dropin.py --no-cache ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; step "$s" 600 python bench.py ${!v:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
