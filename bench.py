@@ -38,10 +38,16 @@ CONFIGS = {
                              "(not a BASELINE config: the acceleration structure on a large layout)"),
 }
 METRIC = "photons/sec + achieved HBM GB/s (% of peak), 200-rect scene, 1/2/4/8 MI355X"
-FP32_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector == FP32 matrix peak on gfx950
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
-# VALU issue ceiling: 256 CUs x 4 SIMDs, one wave64 VALU instruction per SIMD every 4 cycles at 2.4 GHz
-VALU_PEAK_INSTS = 256 * 4 * 2.4e9 / 4
+
+
+def valu_peak():
+    """Measured wave64 VALU issue ceiling of one MI355X (tools/valu_peak.hip -> profiles/valu_peak.json)."""
+    p = os.path.join(REPO, "profiles", "valu_peak.json")
+    try:
+        return float(json.load(open(p))["peak_wave_valu_insts_per_s"])
+    except (OSError, ValueError, KeyError):
+        return None
 
 
 def load_scene(name):
@@ -90,16 +96,15 @@ def pmc_traffic(config_name):
     return d.get("hbm_bytes_per_launch") if "k_bake" in d.get("kernel", "") else None
 
 
-def sq_valu(config_name):
-    """SQ_INSTS_VALU per bake launch from the committed rocprofv3 SQ summary (profiles/), if present."""
+def sq_counters(config_name):
+    """Per-launch SQ counters of the bake from the committed rocprofv3 summary (profiles/sq_issue.json)."""
     p = os.path.join(REPO, "profiles", "sq_issue.json")
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p)).get(config_name, {})
+        return json.load(open(p)).get(config_name, {}).get("per_launch")
     except (OSError, ValueError):
         return None
-    return d.get("per_launch", {}).get("SQ_INSTS_VALU")
 
 
 def main():
@@ -201,6 +206,8 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
+    if st["stream_overflow"]:
+        raise SystemExit(f"stream accumulation overflowed ({st['stream_overflow']} blocks dropped): lightmap invalid")
     span_ms = float(np.mean([s.elapsed_time(x) for s, x in k_ms]))  # whole fmgi_bake_items per step
     tim = ctx.timing()
     bake_launch_ms = tim["bake_ms"] / max(tim["bake_launches"], 1)  # the dominant kernel, per launch
@@ -224,10 +231,8 @@ def main():
         # launch traced (12 B per deposit; the 16 B/texel write-back belongs to fmgi_finalize)
         per_launch_scans = st["scans"] / bake_launches
         per_launch_deps = st["deposits"] / bake_launches
-        flops = 40.0 * per_launch_scans * len(sc.walls) + 150.0 * per_launch_scans
         hbm_bytes = 12.0 * per_launch_deps
         ks = bake_launch_ms / 1e3
-        achieved_tf = flops / ks / 1e12
         achieved_gbs = hbm_bytes / ks / 1e9
         # memory-side atomic adds issued per second by the bake (1 per deposit for the colour-state
         # counters, 3 for int64 RGB); ~20e9/s is the chip's rate for lane-scattered atomics
@@ -236,8 +241,26 @@ def main():
         atomic_rate = per_dep * per_launch_deps / ks
         atomics = {"per_deposit": per_dep, "achieved_per_s": atomic_rate, "ceiling_per_s": 2.0e10,
                    "frac": atomic_rate / 2.0e10}
+        # the bake's own ceiling: instruction issue. SQ counters of this config (profiles/sq_issue.json,
+        # rocprofv3 --pmc) over the live HIP-event kernel time, against the measured VALU ceiling
+        # (profiles/valu_peak.json); SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES x waves per SIMD is the share of
+        # SIMD time some wave of it issues an instruction (any type)
+        sq = sq_counters(args.config) or {}
+        vpeak = valu_peak()
+        issue = None
+        if sq.get("SQ_INSTS_VALU") and vpeak:
+            waves_per_simd = sq["SQ_WAVES"] / (4.0 * torch.cuda.get_device_properties(dev).multi_processor_count)
+            insts = {k: sq.get(f"SQ_INSTS_{k}", 0.0) for k in ("VALU", "SALU", "BRANCH", "VMEM_RD", "LDS")}
+            issue = {"achieved": sq["SQ_INSTS_VALU"] / ks, "peak": vpeak, "unit": "wave-VALU-instr/s",
+                     "frac": sq["SQ_INSTS_VALU"] / ks / vpeak,
+                     "issue_busy_frac": sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"] * waves_per_simd,
+                     "valu_busy_frac": sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"] * waves_per_simd,
+                     "waves_per_simd": waves_per_simd,
+                     "insts_per_launch": insts,
+                     "insts_per_scan_wave": {k: 64.0 * v / per_launch_scans for k, v in insts.items()},
+                     "source": "profiles/sq_issue.json (rocprofv3 --pmc SQ_*), profiles/valu_peak.json (tools/valu_peak)"}
         binding = ("memory-side atomic rate" if atomic_rate > 0.8 * 2.0e10 else
-                   "fp32 VALU (phase-1 filter + exact verification)")
+                   "instruction issue and latency of the per-lane scan/bounce loop (not HBM: see issue)")
         out = {
             "metric": METRIC,
             "value": value,
@@ -266,8 +289,9 @@ def main():
                 else f"dp{world} REHEARSAL ({backend}: ranks share {torch.cuda.device_count()} GPU(s), host reduce)",
             },
             "roofline": {
-                # BASELINE metric: achieved HBM GB/s of the dominant kernel (the bake), algorithmic bytes
-                # per SURVEY.md §8d (12 B per deposit + 16 B per texel written back) / HIP-event kernel time
+                # BASELINE metric: achieved HBM GB/s of the dominant kernel (the bake) as a fraction of the
+                # HBM peak, algorithmic bytes per SURVEY.md §8d (12 B per deposit) / HIP-event kernel time.
+                # The bake is not HBM-bound (it writes 4 B per deposit); `binding` and `issue` say what is.
                 "bound": "hbm",
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
@@ -282,19 +306,11 @@ def main():
                 "algorithmic_bytes_per_launch": hbm_bytes,
                 "binding": binding,
                 "atomics": atomics,
-                # the binding resource: VALU instruction issue (wave-instructions per launch from the committed
-                # SQ_INSTS_VALU profile of this config, over the live HIP-event kernel time)
-                "issue": (None if sq_valu(args.config) is None else {
-                    "achieved": sq_valu(args.config) / ks, "peak": VALU_PEAK_INSTS, "unit": "wave-VALU-instr/s",
-                    "frac": sq_valu(args.config) / ks / VALU_PEAK_INSTS,
-                    "valu_insts_per_launch": sq_valu(args.config),
-                    "source": "profiles/sq_issue.json (rocprofv3 --pmc SQ_INSTS_VALU)"}),
-                "compute": {"achieved": achieved_tf, "peak": FP32_PEAK_TFLOPS, "unit": "TFLOP/s",
-                            "frac": achieved_tf / FP32_PEAK_TFLOPS,
-                            "algorithmic_flops_per_launch": flops,
-                            "note": "SURVEY.md §8d brute-force accounting (40 flops/rect test + 150/scan) of the "
-                                    "linear scan the grid replaces, so frac > 1 measures the algorithmic saving, "
-                                    "not the hardware; the hardware figure is `issue`"},
+                "issue": issue,
+                "ops": {"scans_per_launch": per_launch_scans, "rect_tests_per_launch": st["tests"] / bake_launches,
+                        "rect_tests_per_s": st["tests"] / bake_launches / ks,
+                        "note": "rect tests = phase-1 record tests + exact tests the scans evaluated "
+                                "(the reference's linear scan would do rects x scans)"},
             },
             "per_photon": {
                 "scans": scans / photons_done,

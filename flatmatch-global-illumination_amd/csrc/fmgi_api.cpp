@@ -188,7 +188,9 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
             for (int c = 0; c < 2; c++)
                 fb.img.push_back(j < (int)cls[a][c].size() ? cls[a][c][j] : sentinel);
     }
-    if (fb.img.empty()) fb.img.push_back(sentinel);
+    /* 8 padding pairs: a cooperative lane group reads up to coop - 1 records past the last class
+       (k_bake, filter_axis) and discards them; they stay inside the staged image */
+    for (int k = 0; k < 16; k++) fb.img.push_back(sentinel);
     return fb;
 }
 
@@ -218,6 +220,10 @@ struct GridBuild {
 
 GridBuild build_grid(const FilterBuild &fb) {
     GridBuild gb;
+    /* cells per record the cost model may spend (FMGI_GRID_CPR, experiments: coarser grids are smaller) */
+    int cells_per_record = 16;
+    if (const char *ce = getenv("FMGI_GRID_CPR"))
+        if (atoi(ce) >= 1 && atoi(ce) <= 64) cells_per_record = atoi(ce);
     gb.cells.push_back(GridCell{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0, -1, -1, 0}); /* cell 0: empty */
     std::vector<GridPlane> planes[3][2];
     for (int a = 0; a < 3; a++) {
@@ -271,7 +277,7 @@ GridBuild build_grid(const FilterBuild &fb) {
                 };
                 /* pick the grid minimising the expected records per lookup (uniform hit points over
                    the plane's box), with at most max(16, 16 x records) cells; ties -> fewer cells */
-                const int k = (int)R.size(), cap = std::max(16, 16 * k), mmax = std::min(128, cap);
+                const int k = (int)R.size(), cap = std::max(16, cells_per_record * k), mmax = std::min(128, cap);
                 std::vector<Axis> us, vs;
                 for (int m = 1; m <= mmax; m++)
                     for (int h = 0; h < 2; h++) {
@@ -427,6 +433,8 @@ struct fmgi_context {
     int gimg_bytes = 0;
     int gJ[3] = {0, 0, 0};
     GridCell *d_gcells = nullptr;
+    char *d_gimg_cells = nullptr; /* plane image followed by the cells (FMGI_LDS_CELLS: both staged in LDS) */
+    int gimg_cells_bytes = 0;
     float *d_grecs = nullptr;
     int32_t *d_gidx = nullptr;
     int grid_cells = 0, grid_entries = 0;
@@ -516,6 +524,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_general);
     hipFree(c->d_gimg);
     hipFree(c->d_gcells);
+    hipFree(c->d_gimg_cells);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
     for (hipEvent_t ev : c->ev_pool) hipEventDestroy(ev);
@@ -765,6 +774,18 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->d_gidx = nullptr;
     HIPCHK(upload(&c->d_gimg, gb.img));
     HIPCHK(upload(&c->d_gcells, gb.cells));
+    hipFree(c->d_gimg_cells);
+    c->d_gimg_cells = nullptr;
+    c->gimg_cells_bytes = 0;
+    if (const char *le = getenv("FMGI_LDS_CELLS")) {
+        if (atoi(le) > 0) {
+            std::vector<char> both((size_t)c->gimg_bytes + gb.cells.size() * sizeof(GridCell));
+            memcpy(both.data(), gb.img.data(), (size_t)c->gimg_bytes);
+            memcpy(both.data() + c->gimg_bytes, gb.cells.data(), gb.cells.size() * sizeof(GridCell));
+            HIPCHK(upload(&c->d_gimg_cells, both));
+            c->gimg_cells_bytes = (int)both.size();
+        }
+    }
     HIPCHK(upload(&c->d_grecs, gb.recs));
     HIPCHK(upload(&c->d_gidx, gb.idx));
     }
@@ -963,11 +984,17 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (kernel == FMGI_KERNEL_GRID) {
         a.fimg = c->d_gimg;
         a.fimg_bytes = c->gimg_bytes;
+        if (c->d_gimg_cells && fmgi_bake_lds(kernel, c->accum, block, c->gimg_cells_bytes, nullptr) <= kBakeLdsLimit) {
+            a.fimg = c->d_gimg_cells; /* GridPlane image (16-B multiple), then the cells */
+            a.fimg_bytes = c->gimg_cells_bytes;
+            a.cells_off = c->gimg_bytes;
+        }
         for (int k = 0; k < 3; k++) a.fJ[k] = c->gJ[k];
         a.gcells = c->d_gcells;
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
         a.grid_axes = (c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES")) ? 1 : 0;
+        a.grid_xy_separate = getenv("FMGI_GRID_SEPARATE") ? 1 : 0;
     } else {
         a.fimg = c->d_fimg;
         a.fimg_bytes = c->fimg_bytes;
@@ -982,12 +1009,26 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
     fmgi_bake_lds(kernel, c->accum, block, a.fimg_bytes, &a.ring_off);
+    /* lanes per work item: a launch with fewer items than resident lanes (BASELINE config 1 has 11,008)
+       gives each item a group of up to 8 lanes that split every ScanFast scan's records, so the idle
+       lanes shorten the items' serial photon chains (FMGI_COOP forces a group size: tests) */
+    a.coop = 1;
+    if (kernel == FMGI_KERNEL_FAST && !trace && c->accum == FMGI_ACCUM_STREAM) {
+        if (const char *ce = getenv("FMGI_COOP")) {
+            const int k = atoi(ce);
+            a.coop = (k == 2 || k == 4 || k == 8) ? k : 1;
+        } else {
+            const uint64_t lanes_max = (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block;
+            while (a.coop < 8 && (e - b) * (uint64_t)a.coop * 2 <= lanes_max) a.coop *= 2;
+        }
+        if (a.coop > 1) kernel = FMGI_KERNEL_FAST_COOP;
+    }
     if (c->accum != FMGI_ACCUM_STREAM) {
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid_blocks(c, kernel, c->accum, trace, block, e - b),
-                                block, s));
+        HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace,
+                                grid_blocks(c, kernel, c->accum, trace, block, (e - b) * (uint64_t)a.coop), block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
         if (a.counts)
@@ -1023,7 +1064,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
         const int k = overlap ? (nchunk & 1) : 0; /* one buffer set unless the folds run beside the bakes */
-        const int grid = grid_blocks(c, kernel, c->accum, trace, block, ce - cb);
+        const int grid = grid_blocks(c, kernel, c->accum, trace, block, (ce - cb) * (uint64_t)a.coop);
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));

@@ -76,6 +76,10 @@ struct BakeArgs {
     const float *grecs;
     const int32_t *gridx;
     int grid_axes; /* fJ == {1, 1, 1}: slot a of the image is axis a (ScanGrid's grid_phase1_axes) */
+    int cells_off; /* > 0: the cells follow the plane image in LDS at this byte offset (else global) */
+    int grid_xy_separate; /* layouts: walk the x and y planes one axis after the other (else merged) */
+    int coop;             /* lanes per work item (1, 2, 4, 8; ScanFast only): small launches split each
+                             scan's records over several lanes instead of leaving the GPU mostly idle */
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
     unsigned long long *counts;
     /* AccStream accumulation: deposit codes (texel << 10 | colour state) appended to stream[0..cap) in
@@ -118,6 +122,9 @@ struct StreamBufs {
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);
 
 #define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
+
+/* internal kernel id (not in the C ABI): ScanFast with BakeArgs::coop lanes per work item */
+#define FMGI_KERNEL_FAST_COOP 101
 
 /* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only), 4 = AccStream */
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,

@@ -138,6 +138,7 @@ struct ScanStats {
 /* photonmap.cl:189-206, evaluated literally for every rectangle in index order. */
 struct ScanExact {
     static constexpr bool kLds = false;
+    static constexpr bool kCoop = false;
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float best;
@@ -182,22 +183,29 @@ struct ScanExact {
 template <int A>
 __device__ __forceinline__ float comp(f3 v) { return A == 0 ? v.x : (A == 1 ? v.y : v.z); }
 
-template <int A>
-__device__ __forceinline__ void filter_axis(const char *img, int J, f3 s, f3 d, float &L1, float &L2, int &code1) {
+template <int A, bool Coop>
+__device__ __forceinline__ void filter_axis(const char *img, int J, int sub, int coop, f3 s, f3 d, float &L1,
+                                            float &L2, int &code1) {
     constexpr int U = (A == 0) ? 1 : 0;
     constexpr int V = (A == 2) ? 1 : 2;
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 32), 16);
+    /* every record, in a uniform loop (the LDS reads of 4 records in flight at once): measured faster
+       than a nearest-first walk with an early exit, whose per-lane trip counts diverge. With coop lanes
+       per work item, sub-lane `sub` takes records [sub T, sub T + T) of the class (T uniform; the
+       indices past J read LDS beyond the class and are masked) */
+    const int T = Coop ? (J + coop - 1) / coop : J, j0 = Coop ? sub * T : 0;
 #pragma unroll 4
-    for (int j = 0; j < J; j++) {
+    for (int t = 0; t < T; t++) {
+        const int j = j0 + t;
         const float4 q = p[4 * j];                      /* plane, cu, hwu, cv: ds_read_b128 */
         const float hwv = ((const float *)(p + 4 * j))[4]; /* hwv: ds_read_b32               */
         const float f = (q.x - sa) * rd;
         const float uu = fmaf(du, f, su) - q.y;
         const float vv = fmaf(dv, f, sv) - q.w;
-        const int ok = (int)(f >= 0.0f) & (int)(fabsf(uu) <= q.z) & (int)(fabsf(vv) <= hwv);
+        const int ok = (int)(!Coop || j < J) & (int)(f >= 0.0f) & (int)(fabsf(uu) <= q.z) & (int)(fabsf(vv) <= hwv);
         const float key = ok ? f : INFINITY;
         const bool lt = key < L1;
         L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
@@ -206,15 +214,35 @@ __device__ __forceinline__ void filter_axis(const char *img, int J, f3 s, f3 d, 
     }
 }
 
-struct ScanFast {
+/* merges the phase-1 results (L1, L2, code1) of the coop lanes of a group (butterfly over lane ids):
+   L1 = the minimum key, L2 = the second smallest of all keys, code1 = the winner (the smaller code on
+   equal keys, so every lane of the group ends with the same values; equal keys fail the separation
+   test anyway) */
+__device__ __forceinline__ void coop_merge(int coop, float &L1, float &L2, int &code1) {
+    for (int off = 1; off < coop; off <<= 1) {
+        const float oL1 = __shfl_xor(L1, off, 64), oL2 = __shfl_xor(L2, off, 64);
+        const int oc = __shfl_xor(code1, off, 64);
+        L2 = fminf(fmaxf(L1, oL1), fminf(L2, oL2));
+        const bool take = oL1 < L1 || (oL1 == L1 && oc < code1);
+        code1 = take ? oc : code1;
+        L1 = take ? oL1 : L1;
+    }
+}
+
+/* Coop = true: the kernel for small launches, whose BakeArgs::coop lanes per work item hold the same
+   photon and split every scan's records (the product path for large launches keeps Coop = false) */
+template <bool Coop>
+struct ScanFastT {
     static constexpr bool kLds = true;
+    static constexpr bool kCoop = Coop;
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
-        filter_axis<0>(lds, a.fJ[0], src, dir, L1, L2, code1);
-        filter_axis<1>(lds + 64 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1);
-        filter_axis<2>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1);
+        const int coop = Coop ? a.coop : 1, sub = Coop ? (int)__lane_id() & (coop - 1) : 0;
+        filter_axis<0, Coop>(lds, a.fJ[0], sub, coop, src, dir, L1, L2, code1);
+        filter_axis<1, Coop>(lds + 64 * a.fJ[0], a.fJ[1], sub, coop, src, dir, L1, L2, code1);
+        filter_axis<2, Coop>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], sub, coop, src, dir, L1, L2, code1);
         /* rects that are not axis-aligned: exact order-independent tests (no early-out) */
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;
@@ -226,6 +254,7 @@ struct ScanFast {
             code1 = lt ? ((3 << 16) | g) : code1;
             L1 = lt ? key : L1;
         }
+        if (Coop) coop_merge(coop, L1, L2, code1);
         st.tests += (uint32_t)(a.fJ[0] + a.fJ[1] + a.fJ[2] + a.ngeneral);
         if (L1 == INFINITY) { /* V is a subset of the (empty) phase-1 set: the photon escapes */
             h.best = INFINITY;
@@ -256,6 +285,9 @@ struct ScanFast {
     }
 };
 
+using ScanFast = ScanFastT<false>;
+using ScanFastCoop = ScanFastT<true>;
+
 /*
  * ScanGrid: ScanFast's phase 1 with the rects of each plane bucketed by a 2-D grid.
  *
@@ -273,6 +305,12 @@ __device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, 
     const float tu = fminf(fmaxf((uh - g0.y) * g0.w, 0.0f), g1.y);
     const float tv = fminf(fmaxf((vh - g0.z) * g1.x, 0.0f), g1.z);
     return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)tv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)tu;
+}
+
+/* the grid cells: in LDS after the plane image when the host staged them there (BakeArgs::cells_off),
+   else in global memory */
+__device__ __forceinline__ const GridCell *grid_cells(const BakeArgs &a, const char *img) {
+    return a.cells_off ? (const GridCell *)(img + a.cells_off) : (const GridCell *)a.gcells;
 }
 
 /* one candidate test of ScanGrid's phase 1: record r against hit point (uh, vh) at fac' f */
@@ -310,15 +348,16 @@ __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const GridCel
  * loaded.
  */
 template <int A>
-__device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, int J, f3 s, f3 d, float &L1,
+__device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *lds, int off, int J, f3 s, f3 d, float &L1,
                                           float &L2, int &code1, unsigned &ntest) {
+    const char *img = lds + off;
     constexpr int U = (A == 0) ? 1 : 0;
     constexpr int V = (A == 2) ? 1 : 2;
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 64), 16);
-    const GridCell *cells = (const GridCell *)a.gcells;
+    const GridCell *cells = grid_cells(a, lds);
     int lo = 0, hi = J; /* first plane not behind the photon (padding planes, fac' = NaN, count as not) */
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -336,6 +375,58 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *img, in
         const float4 g2 = p[8 * j + 2], g3 = p[8 * j + 3];
         if (uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y) continue;
         grid_cell_tests(a, cells[grid_cell(g0, p[8 * j + 1], g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
+    }
+}
+
+/* the first plane of a nearest-first class list that is not behind the photon (binary search; padding
+   planes, fac' = NaN, count as not behind), and the fac' of plane j (INFINITY past the list or at padding) */
+__device__ __forceinline__ int grid_first_ahead(const float4 *p, int J, float sa, float rd) {
+    int lo = 0, hi = J;
+    while (lo < hi) {
+        const int mid = (lo + hi) >> 1;
+        if ((p[8 * mid].x - sa) * rd < 0.0f) lo = mid + 1;
+        else hi = mid;
+    }
+    return lo;
+}
+__device__ __forceinline__ float grid_plane_fac(const float4 *p, int j, int J, float sa, float rd) {
+    const float f = j < J ? (p[8 * j].x - sa) * rd : INFINITY;
+    return f >= 0.0f ? f : INFINITY;
+}
+
+/*
+ * Phase 1 of ScanGrid on the x and y planes of a layout together: the two nearest-first class lists a
+ * lane faces are merged by fac', so the walk visits the walls' planes in increasing distance and stops
+ * at the first one (of either axis) past the 2^-11 band above L1. Every plane with fac' in the band is
+ * visited, which is grid_phase1_sorted's exactness argument; a wall hit lowers L1 early, so the far
+ * planes of the other axis are never visited (the per-axis walks visit them until L1 of the floor or
+ * ceiling). x planes: u = y, v = z; y planes: u = x, v = z.
+ */
+__device__ __forceinline__ void grid_xy_merged(const BakeArgs &a, const char *lds, f3 s, f3 d, float &L1, float &L2,
+                                               int &code1, unsigned &ntest) {
+    const int Jx = a.fJ[0], Jy = a.fJ[1];
+    const float rx = __builtin_amdgcn_rcpf(d.x), ry = __builtin_amdgcn_rcpf(d.y);
+    const float4 *px = (const float4 *)__builtin_assume_aligned(lds + (d.x < 0.0f ? 0 : 64), 16);
+    const float4 *py = (const float4 *)__builtin_assume_aligned(lds + 128 * Jx + (d.y < 0.0f ? 0 : 64), 16);
+    const GridCell *cells = grid_cells(a, lds);
+    int jx = grid_first_ahead(px, Jx, s.x, rx), jy = grid_first_ahead(py, Jy, s.y, ry);
+    float fx = grid_plane_fac(px, jx, Jx, s.x, rx), fy = grid_plane_fac(py, jy, Jy, s.y, ry);
+    for (;;) {
+        const bool ux = fx <= fy;
+        const float f = ux ? fx : fy;
+        if (!(f < INFINITY) || f > L1 * 1.00048828125f) break; /* both lists done, or past the band */
+        const float4 *p = ux ? px + 8 * jx : py + 8 * jy;
+        const float uh = fmaf(ux ? d.y : d.x, f, ux ? s.y : s.x), vh = fmaf(d.z, f, s.z);
+        const float4 g2 = p[2], g3 = p[3];
+        if (!(uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y))
+            grid_cell_tests(a, cells[grid_cell(p[0], p[1], g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
+        if (ux) {
+            jx++;
+            fx = grid_plane_fac(px, jx, Jx, s.x, rx);
+        } else {
+            jy++;
+            fy = grid_plane_fac(py, jy, Jy, s.y, ry);
+        }
     }
 }
 
@@ -379,7 +470,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
     }
     FMGI_CX(0, 1) FMGI_CX(2, 3) FMGI_CX(0, 2) FMGI_CX(1, 3) FMGI_CX(1, 2)
 #undef FMGI_CX
-    const GridCell *cells = (const GridCell *)a.gcells;
+    const GridCell *cells = grid_cells(a, img);
     for (int k = 0; k < 4; k++) {
         const float f = fk[k];
         if (!(f < INFINITY) || f > L1 * 1.00048828125f) break; /* 1 + 2^-11 */
@@ -412,7 +503,7 @@ __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *i
     constexpr int V = (A == 2) ? 1 : 2;
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * A + (comp<A>(d) < 0.0f ? 0 : 64), 16);
     const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
-    grid_cell_tests(a, ((const GridCell *)a.gcells)[grid_cell(p[0], p[1], p[2], uh, vh)], f, uh, vh, L1, L2, code1,
+    grid_cell_tests(a, (grid_cells(a, img))[grid_cell(p[0], p[1], p[2], uh, vh)], f, uh, vh, L1, L2, code1,
                     ntest);
 }
 
@@ -436,7 +527,7 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
         const float du = (m == 0) ? d.y : d.x, dv = mz ? d.y : d.z;
         const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * m + (dm < 0.0f ? 0 : 64), 16);
         const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
-        grid_cell_tests(a, ((const GridCell *)a.gcells)[grid_cell(p[0], p[1], p[2], uh, vh)], fm, uh, vh, L1, L2,
+        grid_cell_tests(a, (grid_cells(a, img))[grid_cell(p[0], p[1], p[2], uh, vh)], fm, uh, vh, L1, L2,
                         code1, ntest);
     }
     const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
@@ -447,14 +538,15 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
 
 /* calls fn(idx) for the rect index of every record that passes grid_axis's candidate test */
 template <int A, class F>
-__device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, int J, f3 s, f3 d, F &&fn) {
+__device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, int off, int J, f3 s, f3 d, F &&fn) {
+    const char *img = lds + off;
     constexpr int U = (A == 0) ? 1 : 0;
     constexpr int V = (A == 2) ? 1 : 2;
     const float sa = comp<A>(s), da = comp<A>(d);
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 64), 16);
-    const GridCell *cells = (const GridCell *)a.gcells;
+    const GridCell *cells = grid_cells(a, lds);
     const float4 *recs = (const float4 *)a.grecs;
     for (int j = 0; j < J; j++) {
         const float4 g0 = p[8 * j], g1 = p[8 * j + 1], g2 = p[8 * j + 2];
@@ -473,6 +565,7 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *img, i
 
 struct ScanGrid {
     static constexpr bool kLds = true;
+    static constexpr bool kCoop = false;
     static constexpr int kOrderedRounds = 12;
 
     /*
@@ -488,9 +581,9 @@ struct ScanGrid {
         for (int round = 0; round < kOrderedRounds; round++) {
             int nxt = INT_MAX;
             auto take = [&](int idx) { nxt = (idx > prev && idx < nxt) ? idx : nxt; };
-            grid_visit<0>(a, lds, a.fJ[0], src, dir, take);
-            grid_visit<1>(a, lds + 128 * a.fJ[0], a.fJ[1], src, dir, take);
-            grid_visit<2>(a, lds + 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
+            grid_visit<0>(a, lds, 0, a.fJ[0], src, dir, take);
+            grid_visit<1>(a, lds, 128 * a.fJ[0], a.fJ[1], src, dir, take);
+            grid_visit<2>(a, lds, 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
             for (int g = 0; g < a.ngeneral; g++) {
                 const int idx = a.general[g];
                 if (idx > prev && idx < nxt && exact_on(R, idx, src, dir, INFINITY) >= 0) nxt = idx;
@@ -522,9 +615,13 @@ struct ScanGrid {
             /* floors and ceilings first: in a layout they bound almost every ray, and the x / y walks
                stop at the first plane past L1 (the order of the axes changes neither L1 nor L2; an
                exact tie of keys fails the separation test whatever the order) */
-            grid_axis<2>(a, lds + 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
-            grid_axis<0>(a, lds, a.fJ[0], src, dir, L1, L2, code1, ntest);
-            grid_axis<1>(a, lds + 128 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
+            grid_axis<2>(a, lds, 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, L1, L2, code1, ntest);
+            if (a.grid_xy_separate) { /* FMGI_GRID_SEPARATE (experiments): one walk per axis */
+                grid_axis<0>(a, lds, 0, a.fJ[0], src, dir, L1, L2, code1, ntest);
+                grid_axis<1>(a, lds, 128 * a.fJ[0], a.fJ[1], src, dir, L1, L2, code1, ntest);
+            } else {
+                grid_xy_merged(a, lds, src, dir, L1, L2, code1, ntest);
+            }
         }
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;
@@ -738,6 +835,9 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     uint32_t n_ph = 0, n_dep = 0, n_esc = 0;
     ScanStats sst;
     WaveStream ws;
+    /* BakeArgs::coop lanes per work item (ScanFast splits each scan's records among them; they keep
+       identical photon state): the lead lane fetches, deposits and counts for the group */
+    const bool lead = !Scan::kCoop || ((int)__lane_id() & (a.coop - 1)) == 0;
 
     sst.clk.reset();
     for (;;) {
@@ -749,11 +849,14 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                     a.ev_counts[item - a.item_begin] = nev;
                     a.rng_final[item - a.item_begin] = rng;
                 }
-                if (sst.tests) { /* flush this lane's rect-test count (see ScanStats) */
+                if (sst.tests && lead) { /* flush this lane's rect-test count (see ScanStats) */
                     atomicAdd(a.stats + KSTAT_TESTS, (unsigned long long)sst.tests);
-                    sst.tests = 0;
                 }
-                const uint64_t w = a.item_begin + atomicAdd(a.counter, 1ull);
+                sst.tests = 0;
+                /* one fetch per work item: by the group's lead lane, broadcast to its coop lanes */
+                uint64_t w = lead ? atomicAdd(a.counter, 1ull) : 0ull;
+                if (Scan::kCoop) w = __shfl(w, (int)__lane_id() & ~(a.coop - 1), 64);
+                w += a.item_begin;
                 if (w >= a.item_end) break;
                 item = w;
                 int li;
@@ -834,7 +937,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
             const float two = 2.0f * dot3(hn, dir);
             dir = sub3(dir, mul3(hn, two));
         }
-        Acc::deposit(a, texel, sid, col);
+        if (lead) Acc::deposit(a, texel, sid, col);
         dep = true;
         code = ((uint32_t)texel << 10) | (uint32_t)sid;
         n_dep++;
@@ -855,7 +958,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         depth++;
         }
         sst.clk.lap(ST_HIT);
-        if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, ring, dep, code);
+        if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, ring, dep && lead, code);
         sst.clk.lap(ST_APPEND);
     }
     if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws, ring);
@@ -864,6 +967,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         a.rng_final[item - a.item_begin] = rng;
     }
 
+    if (!lead) n_ph = n_dep = n_esc = sst.tests = sst.ties = sst.invalid = 0; /* counted once per group */
     const unsigned long long v[8] = {n_ph, (unsigned long long)n_dep + n_esc, n_dep, n_esc, sst.tests,
                                      (unsigned long long)sst.ties + sst.invalid, sst.ties, sst.invalid};
     const int slot[8] = {KSTAT_PHOTONS, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_TESTS, KSTAT_RESCANS,
@@ -1053,6 +1157,7 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
         if (accum == 4) return kernel_ptr<ScanGrid, AccStream>(trace);
         return kernel_ptr<ScanGrid, AccFx3>(trace);
     }
+    if (kernel == FMGI_KERNEL_FAST_COOP) return kernel_ptr<ScanFastCoop, AccStream>(false);
     if (kernel == 1) {
         if (accum == 2) return kernel_ptr<ScanFast, AccState>(trace);
         if (accum == 3) return kernel_ptr<ScanFast, AccNone>(trace);
@@ -1089,7 +1194,10 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
     int ring_off = 0;
     const size_t lds = fmgi_bake_lds(kernel, accum, block, a.fimg_bytes, &ring_off);
     if (ring_off != a.ring_off) return hipErrorInvalidValue; /* the caller sets a.ring_off from fmgi_bake_lds */
-    if (kernel == 2) { /* FMGI_KERNEL_GRID */
+    if (kernel == FMGI_KERNEL_FAST_COOP) {
+        if (accum != 4 || trace) return hipErrorInvalidValue; /* cooperative lanes: stream accumulation only */
+        launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
+    } else if (kernel == 2) { /* FMGI_KERNEL_GRID */
         if (accum == 2) launch3<ScanGrid, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanGrid, AccNone>(a, trace, grid, blk, lds, s);
         else if (accum == 4) launch3<ScanGrid, AccStream>(a, trace, grid, blk, lds, s);

@@ -174,3 +174,28 @@ def test_apartment30_lightmap_prefix_exact(torch_cuda, apartment30, offsets, ker
         olm, _ = O.bake(apartment30, L, b, e)
         assert np.array_equal(lm[:, :3], olm), (b, e)
     ctx.close()
+
+
+@pytest.mark.parametrize("coop", ["2", "4", "8"])
+def test_cooperative_lanes_config1_exact(torch_cuda, example_scene, offsets, coop):
+    """Small launches give each work item a group of lanes that split ScanFast's records (BakeArgs::coop,
+    chosen automatically below the GPU's resident lanes): forced group sizes give the oracle's lightmap
+    and counters bit for bit, on config 1 and on a ragged 1,001-item range."""
+    spa = 65_000
+    L = O.schedule_with_offsets(example_scene, spa, offsets)
+    olm, ost = O.bake(example_scene, L)
+    olm2, _ = O.bake(example_scene, L, 3, 1004)
+    os.environ["FMGI_COOP"] = coop
+    try:
+        ctx = _ctx(example_scene, spa, offsets)
+        ctx.reset_stats()
+        lm = _bake_gpu(torch_cuda, ctx, 0, ctx.total_items, fmgi.KERNEL_FAST)
+        st = ctx.stats()
+        lm2 = _bake_gpu(torch_cuda, ctx, 3, 1004, fmgi.KERNEL_FAST)
+        ctx.close()
+    finally:
+        os.environ.pop("FMGI_COOP", None)
+    assert np.array_equal(lm[:, :3], olm)
+    assert np.array_equal(lm2[:, :3], olm2)
+    for k in ("photons", "scans", "deposits", "escapes"):
+        assert st[k] == ost[k], k

@@ -7,6 +7,7 @@
 #   ocml             the device library's sin/cos digest (tests/golden/make_ocml_fixture.py)
 #   valu             VALU issue ceilings (tools/valu_peak)
 #   dropin           drop-in boundary timing, cached and uncached (tools/bench_dropin.py)
+#   dropinprof       the same under rocprofv3 --kernel-trace --stats
 #   bench            python bench.py $BENCH_ARGS
 #   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
 #   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
@@ -37,6 +38,7 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     ocml)  step ocml 300 python tests/golden/make_ocml_fixture.py "$OUT" ;;
     valu)  step valu 120 ./tools/valu_peak ;;
     dropin) step dropin 600 python tools/bench_dropin.py && step dropin_nocache 600 python tools/bench_dropin.py --no-cache ;;
+    dropinprof) step dropinprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/dropinprof" -o run --output-format csv -- python tools/bench_dropin.py --reps 2 ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
     bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; step "$s" 600 python bench.py ${!v:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
