@@ -72,6 +72,17 @@ __device__ __forceinline__ float exact_on(cptr<RectDev> R, int i, f3 src, f3 dir
                            dir, closest);
 }
 
+/* exact_on for the rare paths of the fast and grid scans (fallbacks, non-axis-aligned rects): the index
+   is made a per-lane (VGPR) value, so the record comes in with vector loads. Scalar loads of a 64-B
+   record per test would reserve a block of SGPRs in the whole kernel, whose pressure then spills the
+   hot loop's SGPRs into VGPR lanes. */
+__device__ __forceinline__ float exact_on_v(const RectDev *R, int i, f3 src, f3 dir, float closest) {
+    asm volatile("" : "+v"(i));
+    const RectDev &r = R[i];
+    return intersect_exact(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz), mkf3(r.wnx, r.wny, r.wnz), r.wl,
+                           mkf3(r.hnx, r.hny, r.hnz), r.hl, src, dir, closest);
+}
+
 /* The scan's result and what the deposit needs of the hit rect, read once (phase 2 of the fast scans
    evaluates the winner exactly; the hit stage reuses its in-rect coordinates, see intersect_exact_uv). */
 struct HitRec {
@@ -142,16 +153,19 @@ struct ScanExact {
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float best;
-        const int hit = literal(a, lds, src, dir, best, st);
+        const int hit = literal<true>(a, lds, src, dir, best, st);
         finish_hit(a, hit, best, src, dir, h);
     }
+    /* Scalar: records through scalar loads (the exact kernel's own uniform loop); else vector loads (the
+       other scans' rare fallback) */
+    template <bool Scalar = false>
     static __device__ __forceinline__ int literal(const BakeArgs &a, const char *, f3 src, f3 dir, float &best,
                                                   ScanStats &st) {
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         float bestd = INFINITY;
         int hit = -1;
         for (int i = 0; i < a.nrects; i++) {
-            const float d = exact_on(R, i, src, dir, bestd);
+            const float d = Scalar ? exact_on(R, i, src, dir, bestd) : exact_on_v(a.rects, i, src, dir, bestd);
             if (d < 0) continue;
             if (d < bestd) { bestd = d; hit = i; }
         }
@@ -244,10 +258,9 @@ struct ScanFastT {
         filter_axis<1, Coop>(lds + 64 * a.fJ[0], a.fJ[1], sub, coop, src, dir, L1, L2, code1);
         filter_axis<2, Coop>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], sub, coop, src, dir, L1, L2, code1);
         /* rects that are not axis-aligned: exact order-independent tests (no early-out) */
-        cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;
         for (int g = 0; g < a.ngeneral; g++) {
-            const float f = exact_on(R, G[g], src, dir, INFINITY);
+            const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
             L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
@@ -575,7 +588,6 @@ struct ScanGrid {
      * candidate index by re-walking the cells (typically 2-3 candidates: a tie on a shared edge).
      */
     static __device__ int ordered_exact(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best) {
-        cptr<RectDev> R = (cptr<RectDev>)a.rects;
         int prev = -1, hit = -1;
         float closest = INFINITY;
         for (int round = 0; round < kOrderedRounds; round++) {
@@ -586,13 +598,13 @@ struct ScanGrid {
             grid_visit<2>(a, lds, 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
             for (int g = 0; g < a.ngeneral; g++) {
                 const int idx = a.general[g];
-                if (idx > prev && idx < nxt && exact_on(R, idx, src, dir, INFINITY) >= 0) nxt = idx;
+                if (idx > prev && idx < nxt && exact_on_v(a.rects, idx, src, dir, INFINITY) >= 0) nxt = idx;
             }
             if (nxt == INT_MAX) {
                 best = closest;
                 return hit;
             }
-            const float d = exact_on(R, nxt, src, dir, closest);
+            const float d = exact_on_v(a.rects, nxt, src, dir, closest);
             if (d >= 0 && d < closest) {
                 closest = d;
                 hit = nxt;
@@ -623,10 +635,9 @@ struct ScanGrid {
                 grid_xy_merged(a, lds, src, dir, L1, L2, code1, ntest);
             }
         }
-        cptr<RectDev> R = (cptr<RectDev>)a.rects;
         cptr<int32_t> G = (cptr<int32_t>)a.general;
         for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
-            const float f = exact_on(R, G[g], src, dir, INFINITY);
+            const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
             L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
