@@ -113,7 +113,7 @@ def main():
     ap.add_argument("--steps", type=int, default=5)
     ap.add_argument("--warmup", type=int, default=1)
     ap.add_argument("--config", default="box200", choices=sorted(CONFIGS))
-    ap.add_argument("--kernel", default="auto", choices=["auto", "grid", "fast", "exact"])
+    ap.add_argument("--kernel", default="auto", choices=["auto", "grid", "fast", "exact", "hybrid"])
     ap.add_argument("--accum", default="auto", choices=["auto", "fx3", "state", "stream", "none"],
                     help="none = PROFILING ONLY (deposits discarded; lightmap wrong)")
     ap.add_argument("--no-cpu-baseline", action="store_true")
@@ -151,7 +151,7 @@ def main():
     spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
     spa = min(spa, 2**31 - 1)
     kernel = {"auto": fmgi.KERNEL_AUTO, "grid": fmgi.KERNEL_GRID, "fast": fmgi.KERNEL_FAST,
-              "exact": fmgi.KERNEL_EXACT}[args.kernel]
+              "exact": fmgi.KERNEL_EXACT, "hybrid": fmgi.KERNEL_HYBRID}[args.kernel]
 
     ctx = fmgi.Context(device_index)
     ctx.set_accumulation({"auto": fmgi.ACCUM_AUTO, "fx3": fmgi.ACCUM_FX3, "state": fmgi.ACCUM_STATE,
@@ -281,7 +281,7 @@ def main():
                 "texels": int(sc.num_texels),
                 "spa": spa,
                 "photons_per_step": photons_per_step,
-                "kernel": {0: "exact", 1: "fast", 2: "grid"}[kernel if kernel != fmgi.KERNEL_AUTO else ctx.auto_kernel]
+                "kernel": {0: "exact", 1: "fast", 2: "grid", 4: "hybrid"}[kernel if kernel != fmgi.KERNEL_AUTO else ctx.auto_kernel]
                 + (" (auto)" if kernel == fmgi.KERNEL_AUTO else ""),
                 "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)",
                                  4: "stream"}[ctx.accumulation],

@@ -434,6 +434,8 @@ struct fmgi_context {
     int gJ[3] = {0, 0, 0};
     GridCell *d_gcells = nullptr;
     char *d_gimg_cells = nullptr; /* plane image followed by the cells (FMGI_LDS_CELLS: both staged in LDS) */
+    char *d_himg = nullptr;       /* ScanHybrid: the filter image followed by the grid's plane image */
+    int himg_bytes = 0;
     int gimg_cells_bytes = 0;
     float *d_grecs = nullptr;
     int32_t *d_gidx = nullptr;
@@ -525,6 +527,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_gimg);
     hipFree(c->d_gcells);
     hipFree(c->d_gimg_cells);
+    hipFree(c->d_himg);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
     for (hipEvent_t ev : c->ev_pool) hipEventDestroy(ev);
@@ -676,13 +679,19 @@ static int bake_block() {
    image, identical results) */
 static const size_t kBakeLdsLimit = 65536;
 
+static int image_bytes(const fmgi_context *c, int kernel) {
+    return kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : (kernel == FMGI_KERNEL_HYBRID ? c->himg_bytes : c->fimg_bytes);
+}
+
 static bool kernel_fits(const fmgi_context *c, int kernel, int accum, int block) {
     if (kernel == FMGI_KERNEL_EXACT) return true;
-    const int img = kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : c->fimg_bytes;
+    const int img = image_bytes(c, kernel);
     return fmgi_bake_lds(kernel, accum, block, img, nullptr) <= kBakeLdsLimit;
 }
 
 static int fitting_kernel(const fmgi_context *c, int kernel, int accum, int block) {
+    if (kernel_fits(c, kernel, accum, block)) return kernel;
+    if (kernel == FMGI_KERNEL_HYBRID) kernel = FMGI_KERNEL_FAST;
     if (kernel_fits(c, kernel, accum, block)) return kernel;
     const int other = kernel == FMGI_KERNEL_GRID ? FMGI_KERNEL_FAST : FMGI_KERNEL_GRID;
     if (kernel != FMGI_KERNEL_EXACT && kernel_fits(c, other, accum, block)) return other;
@@ -722,6 +731,9 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
         c->auto_kernel = (4 * slots < pairs) ? FMGI_KERNEL_GRID : FMGI_KERNEL_FAST;
+        /* layouts: floors and ceilings through the grid, walls through the filter (example.png: 3.80e9
+           vs 3.65e9 photons/s FAST, 3.02e9 GRID) when the floor/ceiling records share few planes */
+        if (c->auto_kernel == FMGI_KERNEL_FAST && 4 * gb.J[2] < fb.J[2]) c->auto_kernel = FMGI_KERNEL_HYBRID;
         /* the largest LDS use (STREAM rings) decides, so the choice holds for every accumulation mode */
         c->auto_kernel = fitting_kernel(c, c->auto_kernel, FMGI_ACCUM_STREAM, bake_block());
     }
@@ -774,6 +786,15 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->d_gidx = nullptr;
     HIPCHK(upload(&c->d_gimg, gb.img));
     HIPCHK(upload(&c->d_gcells, gb.cells));
+    {   /* ScanHybrid's image: the filter image (a multiple of 64 B), then the plane image */
+        std::vector<char> both((size_t)c->fimg_bytes + (size_t)c->gimg_bytes);
+        memcpy(both.data(), fb.img.data(), (size_t)c->fimg_bytes);
+        memcpy(both.data() + c->fimg_bytes, gb.img.data(), (size_t)c->gimg_bytes);
+        hipFree(c->d_himg);
+        c->d_himg = nullptr;
+        HIPCHK(upload(&c->d_himg, both));
+        c->himg_bytes = (int)both.size();
+    }
     hipFree(c->d_gimg_cells);
     c->d_gimg_cells = nullptr;
     c->gimg_cells_bytes = 0;
@@ -892,9 +913,7 @@ FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
     return n;
 }
 
-static int lds_bytes(const fmgi_context *c, int kernel) {
-    return kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : c->fimg_bytes;
-}
+static int lds_bytes(const fmgi_context *c, int kernel) { return image_bytes(c, kernel); }
 
 static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, uint64_t items) {
     /* persistent grid: exactly the blocks that are resident at once (occupancy from the VGPR/SGPR/LDS
@@ -955,7 +974,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (e > c->total_items || b > e) return set_err(FMGI_ERR_ARG, "item range [%llu,%llu) outside plan of %llu items",
                                                   (unsigned long long)b, (unsigned long long)e,
                                                   (unsigned long long)c->total_items);
-    if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_AUTO) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
+    if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_HYBRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     if (kernel == FMGI_KERNEL_AUTO) kernel = c->auto_kernel;
     const int block = bake_block();
     kernel = fitting_kernel(c, kernel, c->accum, block); /* an image too large for LDS: same results, other scan */
@@ -995,6 +1014,18 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.gridx = c->d_gidx;
         a.grid_axes = (c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES")) ? 1 : 0;
         a.grid_xy_separate = getenv("FMGI_GRID_SEPARATE") ? 1 : 0;
+    } else if (kernel == FMGI_KERNEL_HYBRID) {
+        a.fimg = c->d_himg;
+        a.fimg_bytes = c->himg_bytes;
+        a.hyb_off = c->fimg_bytes;
+        for (int k = 0; k < 3; k++) {
+            a.fJ[k] = c->fJ[k];
+            a.gJ[k] = c->gJ[k];
+        }
+        a.gcells = c->d_gcells;
+        a.grecs = c->d_grecs;
+        a.gridx = c->d_gidx;
+        a.grid_code_or = 0x40000000;
     } else {
         a.fimg = c->d_fimg;
         a.fimg_bytes = c->fimg_bytes;
@@ -1465,6 +1496,7 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     if (k_env && !strcmp(k_env, "grid")) kernel = FMGI_KERNEL_GRID;
     if (k_env && !strcmp(k_env, "exact")) kernel = FMGI_KERNEL_EXACT;
     if (k_env && !strcmp(k_env, "fast")) kernel = FMGI_KERNEL_FAST;
+    if (k_env && !strcmp(k_env, "hybrid")) kernel = FMGI_KERNEL_HYBRID;
     /* the reference schedule and its rand() calls first, before the HIP runtime can draw from rand() */
     std::vector<int32_t> offs;
     uint64_t items = 0;

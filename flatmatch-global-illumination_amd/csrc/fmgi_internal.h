@@ -78,6 +78,9 @@ struct BakeArgs {
     int grid_axes; /* fJ == {1, 1, 1}: slot a of the image is axis a (ScanGrid's grid_phase1_axes) */
     int cells_off; /* > 0: the cells follow the plane image in LDS at this byte offset (else global) */
     int grid_xy_separate; /* layouts: walk the x and y planes one axis after the other (else merged) */
+    int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
+    int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
+    int grid_code_or;     /* ScanHybrid: flag or-ed into the codes of grid records (rect indices)    */
     int coop;             /* lanes per work item (1, 2, 4, 8; ScanFast only): small launches split each
                              scan's records over several lanes instead of leaving the GPU mostly idle */
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */

@@ -342,12 +342,12 @@ __device__ __forceinline__ void grid_rec(float f, float uh, float vh, float4 r, 
 __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const GridCell &c, float f, float uh, float vh,
                                                 float &L1, float &L2, int &code1, unsigned &ntest) {
     ntest += (unsigned)c.count;
-    grid_rec(f, uh, vh, make_float4(c.cu0, c.hwu0, c.cv0, c.hwv0), c.idx0, L1, L2, code1);
-    grid_rec(f, uh, vh, make_float4(c.cu1, c.hwu1, c.cv1, c.hwv1), c.idx1, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(c.cu0, c.hwu0, c.cv0, c.hwv0), c.idx0 | a.grid_code_or, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(c.cu1, c.hwu1, c.cv1, c.hwv1), c.idx1 | a.grid_code_or, L1, L2, code1);
     if (c.count > 2) {
         const float4 *recs = (const float4 *)a.grecs;
         for (int k = 2; k < c.count; k++)
-            grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2], L1, L2, code1);
+            grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2] | a.grid_code_or, L1, L2, code1);
     }
 }
 
@@ -665,6 +665,65 @@ struct ScanGrid {
         if (r == -2) r = ScanExact::literal(a, lds, src, dir, best, st);
         finish_hit(a, r, best, src, dir, h);
         st.clk.lap(ST_FALLBACK);
+    }
+};
+
+/*
+ * ScanHybrid: the reference's apartment layouts have few floor/ceiling planes holding many records
+ * (one floor and one ceiling rect per room) and walls on many planes. Phase 1 takes the floor/ceiling
+ * axis through ScanGrid's cells (one cell lookup instead of a filter pass over every room's floor) and
+ * the walls through ScanFast's uniform filter loop. The candidate set is the union of the two scans'
+ * candidate sets and the keys are theirs, so phase 2, the separation test and the fallback are
+ * ScanFast's. Grid candidates carry the rect index with the 0x40000000 flag (BakeArgs::grid_code_or).
+ */
+struct ScanHybrid {
+    static constexpr bool kLds = true;
+    static constexpr bool kCoop = false;
+    static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
+                                                ScanStats &st) {
+        float L1 = INFINITY, L2 = INFINITY;
+        int code1 = -1;
+        unsigned ntest = 0;
+        grid_axis<2>(a, lds + a.hyb_off, 128 * (a.gJ[0] + a.gJ[1]), a.gJ[2], src, dir, L1, L2, code1, ntest);
+        filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
+        filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
+        cptr<int32_t> G = (cptr<int32_t>)a.general;
+        for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
+            const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
+            const float key = (f < 0) ? INFINITY : f;
+            const bool lt = key < L1;
+            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+            code1 = lt ? ((3 << 16) | g) : code1;
+            L1 = lt ? key : L1;
+        }
+        st.tests += ntest + (uint32_t)(a.fJ[0] + a.fJ[1] + a.ngeneral);
+        if (L1 == INFINITY) {
+            h.best = INFINITY;
+            h.idx = -1;
+            return;
+        }
+        int idx;
+        if (code1 & 0x40000000) {
+            idx = code1 & 0x3FFFFFFF;
+        } else {
+            const int A = code1 >> 16, j = code1 & 0xFFFF;
+            if (A == 3) {
+                idx = a.general[j];
+            } else {
+                const float dA = A == 0 ? dir.x : dir.y;
+                const int off = A == 0 ? 0 : 64 * a.fJ[0];
+                idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
+            }
+        }
+        const float f = exact_hit(a, idx, src, dir, h);
+        if (!(f < 0) && L2 > f * 1.000244140625f) { /* ScanFast's separation test */
+            h.best = f;
+            return;
+        }
+        if (f < 0) st.invalid++; else st.ties++;
+        float best;
+        const int hit = ScanExact::literal(a, lds, src, dir, best, st);
+        finish_hit(a, hit, best, src, dir, h);
     }
 };
 
@@ -1169,6 +1228,12 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
         return kernel_ptr<ScanGrid, AccFx3>(trace);
     }
     if (kernel == FMGI_KERNEL_FAST_COOP) return kernel_ptr<ScanFastCoop, AccStream>(false);
+    if (kernel == 4) {
+        if (accum == 2) return kernel_ptr<ScanHybrid, AccState>(trace);
+        if (accum == 3) return kernel_ptr<ScanHybrid, AccNone>(trace);
+        if (accum == 4) return kernel_ptr<ScanHybrid, AccStream>(trace);
+        return kernel_ptr<ScanHybrid, AccFx3>(trace);
+    }
     if (kernel == 1) {
         if (accum == 2) return kernel_ptr<ScanFast, AccState>(trace);
         if (accum == 3) return kernel_ptr<ScanFast, AccNone>(trace);
@@ -1208,6 +1273,11 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
     if (kernel == FMGI_KERNEL_FAST_COOP) {
         if (accum != 4 || trace) return hipErrorInvalidValue; /* cooperative lanes: stream accumulation only */
         launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
+    } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
+        if (accum == 2) launch3<ScanHybrid, AccState>(a, trace, grid, blk, lds, s);
+        else if (accum == 3) launch3<ScanHybrid, AccNone>(a, trace, grid, blk, lds, s);
+        else if (accum == 4) launch3<ScanHybrid, AccStream>(a, trace, grid, blk, lds, s);
+        else launch3<ScanHybrid, AccFx3>(a, trace, grid, blk, lds, s);
     } else if (kernel == 2) { /* FMGI_KERNEL_GRID */
         if (accum == 2) launch3<ScanGrid, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanGrid, AccNone>(a, trace, grid, blk, lds, s);

@@ -20,7 +20,7 @@ import numpy as np
 from . import scene
 
 HOST_ONLY = -1  # FMGI_HOST_ONLY: a context without a device (scene checks and planning only)
-from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, RadStats, Timing, FmgiError, Geometry, Stats,
+from ._lib import (ACCUM_AUTO, ACCUM_FX3, ACCUM_NONE, ACCUM_STATE, ACCUM_STREAM, KERNEL_AUTO, KERNEL_EXACT, KERNEL_FAST, KERNEL_GRID, KERNEL_HYBRID, RadStats, Timing, FmgiError, Geometry, Stats,
                    check, load)
 from .scene import RECT_DTYPE, Scene
 

@@ -61,6 +61,7 @@ EXPORTS = (
 KERNEL_EXACT = 0
 KERNEL_FAST = 1
 KERNEL_GRID = 2
+KERNEL_HYBRID = 4
 KERNEL_AUTO = 3
 ACCUM_AUTO = 0
 ACCUM_FX3 = 1

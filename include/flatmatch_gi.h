@@ -137,8 +137,9 @@ enum {
 };
 
 /* Scan kernels (identical bits): EXACT = photonmap.cl's scan over every rect; FAST = conservative fp32
-   filter over every rect + exact verification; GRID = FAST's filter over per-plane grid cells only. */
-enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2, FMGI_KERNEL_AUTO = 3 };
+   filter over every rect + exact verification; GRID = FAST's filter over per-plane grid cells only;
+   HYBRID = GRID's cells for the floor/ceiling planes and FAST's filter for the walls. */
+enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2, FMGI_KERNEL_AUTO = 3, FMGI_KERNEL_HYBRID = 4 };
 /* AUTO = GRID when the scene has few planes for its rect count (closed boxes), else FAST. */
 /* Deposit accumulation (both exact and order-free; results are identical):
    FX3   three int64 fixed-point atomics per deposit into the lightmap;

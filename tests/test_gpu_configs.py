@@ -21,7 +21,7 @@ from conftest import GOLDEN
 
 pytestmark = pytest.mark.gpu
 
-KERNELS = [fmgi.KERNEL_EXACT, fmgi.KERNEL_FAST, fmgi.KERNEL_GRID]
+KERNELS = [fmgi.KERNEL_EXACT, fmgi.KERNEL_FAST, fmgi.KERNEL_GRID, fmgi.KERNEL_HYBRID]
 
 
 @pytest.fixture(scope="module")
