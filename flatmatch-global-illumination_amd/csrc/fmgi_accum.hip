@@ -104,7 +104,12 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
     unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
-    const int t = blockIdx.x / G, g = blockIdx.x % G;
+    /* XCD-aware order: the dispatcher deals workgroups to the 8 XCDs round-robin (workgroup i -> XCD
+       i % 8), so XCD x gets groups g = x, x + 8, ... and, within a group, consecutive tiles back to
+       back: the runs of neighbouring tiles share the cache lines at their boundaries, and those reads
+       now meet in one L2. G is a multiple of 8 (fmgi_stream_fold). */
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3;
+    const int t = j % P, g = xcd + 8 * (j / P);
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
     const uint64_t ns = (n + kSlice - 1) / kSlice;
     const uint64_t b_lo = ns * g / G, b_hi = ns * (g + 1) / G;
@@ -158,7 +163,8 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
     const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 64 KiB: two workgroups per CU */
     hipError_t e = fmgi_set_lds_attr_once<0>((const void *)k_tile_runs, (int)lds);
     if (e != hipSuccess) return e;
-    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * sb.groups)), dim3(sb.block > 0 ? sb.block : 1024), lds, s, sb.sorted, sb.toff,
-                       sb.cursor, sb.cap, P, sb.groups, (const uint4 *)sb.colpack, lm, num_texels);
+    const int G = (sb.groups + 7) & ~7; /* a multiple of 8 for k_tile_runs' XCD-aware order */
+    hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), lds, s, sb.sorted, sb.toff,
+                       sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
     return hipGetLastError();
 }
