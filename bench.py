@@ -84,6 +84,41 @@ def cpu_baseline(sc, spa, target_s=10.0):
     }
 
 
+def cpu_baseline_reference(sc, target_s=10.0):
+    """The reference's own CPU photon mapper, performPhotonMappingNative (photonmap.c:408-435: one core,
+    BSP-tree scan, one photon per sample), built from /root/reference by oracle/build_ref.sh into
+    oracle/_ref/photon_ref and timed on this host on a bounded sample of the same scene (its RNG is libc
+    rand(), so it is a timing baseline, not a parity reference). None if the build is absent."""
+    import subprocess
+    import tempfile
+
+    from fmgi import scene as S
+
+    exe = os.path.join(REPO, "oracle", "_ref", "photon_ref")
+    if not os.path.exists(exe):
+        return None
+    with tempfile.TemporaryDirectory() as d:
+        g = os.path.join(d, "geometry.bin")
+        S.save_geometry(sc, g)
+
+        def run(spa):
+            out = subprocess.run([exe, g, str(spa)], capture_output=True, text=True, timeout=120, check=True).stdout
+            return json.loads(out.strip().splitlines()[-1])
+
+        area = sum(float(S._len(x["width"][:3]) * S._len(x["height"][:3])) for x in sc.sources)
+        r = run(max(1, int(2e4 / max(area, 1e-6))))  # ~2e4 photons: calibration
+        rate = r["photons"] / max(r["seconds"], 1e-6)
+        r = run(max(1, int(target_s * rate / max(area, 1e-6))))
+    return {
+        "value": r["photons"] / r["seconds"],
+        "unit": "photons/s",
+        "cores": 1,
+        "kind": "reference",
+        "sample": f"the reference's performPhotonMappingNative (oracle/_ref/photon_ref, built from /root/reference) "
+                  f"on {r['photons']} photons of the same scene in {r['seconds']:.1f} s, one core",
+    }
+
+
 def pmc_traffic(config_name):
     """HBM bytes per bake launch from the committed rocprofv3 PMC summary (profiles/), if present."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -331,7 +366,10 @@ def main():
             out["stage_cycles_frac"] = {n: cyc[k] / tot for k, n in enumerate(names)}
             out["note"] = "PROFILING BUILD (s_memtime per stage): value is not a valid bench number"
         if world == 1 and not args.no_cpu_baseline:
-            out["cpu_baseline"] = cpu_baseline(sc, cfg["spa"], args.cpu_seconds)
+            port = cpu_baseline(sc, cfg["spa"], args.cpu_seconds)
+            ref = cpu_baseline_reference(sc, args.cpu_seconds)
+            out["cpu_baseline"] = ref if ref is not None else port
+            out["cpu_baseline_port"] = port  # the CPU oracle on the GPU box's cores, same schedule
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

@@ -11,6 +11,8 @@
 #                                oracle/dump_geometry.c; turns a layout PNG into a geometry fixture.
 #   _ref/ao_ref                  reference photonmap.c/rectangle.c/vector3_cl.c/geoSphere.c + oracle/ao_ref_main.c:
 #                                performAmbientOcclusionNative on a geometry fixture (AO fixtures).
+#   _ref/photon_ref              reference photonmap.o/rectangle.o/vector3_cl.o + oracle/photon_ref_main.c:
+#                                performPhotonMappingNative timed on a geometry fixture (bench CPU baseline).
 #   _ref/rad_ref                 reference radiosityNative.o/rectangle.o/vector3_cl.o + oracle/rad_ref_main.c:
 #                                performRadiosityNative on a geometry fixture (radiosity fixtures).
 #   _ref/out_ref                 main.c:66-79 normalisation + the reference's saveAs()/read_png_file()
@@ -56,6 +58,10 @@ gcc -o "$OUT/dump_geometry" "$OUT/obj/dump_geometry.o" $COMMON "$PNG_SO" -lm
 # Ambient-occlusion reference: the reference's performAmbientOcclusionNative on a geometry fixture.
 gcc $CFLAGS -c "$HERE/ao_ref_main.c" -o "$OUT/obj/ao_ref_main.o"
 gcc -o "$OUT/ao_ref" "$OUT/obj/ao_ref_main.o" "$OUT/obj/photonmap.o" "$OUT/obj/geoSphere.o" $COMMON "$PNG_SO" -lm
+
+# CPU photon-mapping reference (bench.py's cpu_baseline): the reference's performPhotonMappingNative, timed.
+gcc $CFLAGS -c "$HERE/photon_ref_main.c" -o "$OUT/obj/photon_ref_main.o"
+gcc -o "$OUT/photon_ref" "$OUT/obj/photon_ref_main.o" "$OUT/obj/photonmap.o" "$OUT/obj/geoSphere.o" $COMMON "$PNG_SO" -lm
 
 # Radiosity reference: the reference's performRadiosityNative on a geometry fixture, seeded rand().
 gcc $CFLAGS -c "$HERE/rad_ref_main.c" -o "$OUT/obj/rad_ref_main.o"
