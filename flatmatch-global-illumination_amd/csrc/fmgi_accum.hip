@@ -153,10 +153,110 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
     }
 }
 
+/* The fold of a presorted stream (BakeArgs::presort): every FMGI_RING_CODES-code segment already holds
+   its codes sorted by tile with the run offsets in toff, so one workgroup per (tile, group of segments)
+   reads its tile's run of every segment directly. A wave takes 4 segments at a time, 16 lanes each
+   (runs average FMGI_RING_CODES / P codes); the sums are k_tile_runs' (int64 R, G - R, B - R in LDS). */
+__global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restrict__ stream,
+                                                       const uint16_t *__restrict__ toff,
+                                                       const unsigned long long *__restrict__ n_ptr, uint64_t cap,
+                                                       int P, int G, const uint4 *__restrict__ colpack,
+                                                       unsigned long long *__restrict__ lm, int num_texels) {
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
+    unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
+    uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
+    const int t = j % P, g = xcd + 8 * (j / P);
+    const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
+    const uint64_t ns = n / FMGI_RING_CODES; /* reserved blocks are whole numbers of segments */
+    const uint64_t s_lo = ns * g / G, s_hi = ns * (g + 1) / G;
+    if (s_lo >= s_hi) return; /* uniform */
+    for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
+    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
+    __syncthreads();
+    /* a wave takes kW segments at a time and packs their runs for tile t onto its 64 lanes: lane L < kW
+       reads segment L's run bounds, a wave prefix sum gives each run's first packed index, and packed
+       index i maps back to its code with kW - 1 uniform compares (runs average n / (segments * P) codes,
+       far fewer than 64, so one lane per run would leave most lanes idle on the LDS atomics). The next
+       group's run bounds are loaded before this group's codes are folded. */
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int waves = blockDim.x >> 6;
+    constexpr int kW = 16;
+    auto bounds = [&](uint64_t s0, int &r0, int &len) {
+        r0 = 0, len = 0;
+        if (lane < kW && s0 + lane < s_hi) {
+            const uint16_t *to = toff + (s0 + lane) * (uint64_t)(P + 1);
+            r0 = to[t];
+            len = (int)to[t + 1] - r0;
+        }
+    };
+    int nr0, nlen;
+    bounds(s_lo + kW * (uint64_t)wave, nr0, nlen);
+    for (uint64_t s0 = s_lo + kW * (uint64_t)wave; s0 < s_hi; s0 += kW * (uint64_t)waves) {
+        const int r0 = nr0, len = nlen;
+        bounds(s0 + kW * (uint64_t)waves, nr0, nlen);
+        int pre = len; /* inclusive prefix over lanes 0..kW-1 */
+#pragma unroll
+        for (int d = 1; d < kW; d <<= 1) {
+            const int o = __shfl_up(pre, d, 64);
+            if (lane >= d) pre += o;
+        }
+        const int total = __builtin_amdgcn_readlane(pre, kW - 1);
+        /* packed index i of run j (i in [start_j, start_j + len_j)) reads run_base + j*1024 + r0_j + i - start_j */
+        const int shift_l = lane * FMGI_RING_CODES + r0 - (pre - len);
+        int start[kW], shift[kW];
+#pragma unroll
+        for (int j = 0; j < kW; j++) {
+            start[j] = __builtin_amdgcn_readlane(pre - len, j);
+            shift[j] = __builtin_amdgcn_readlane(shift_l, j);
+        }
+        const uint32_t *run = stream + s0 * FMGI_RING_CODES;
+        for (int i0 = lane; i0 < total; i0 += 4 * 64) {
+            uint32_t v[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int i = i0 + 64 * u;
+                int sh = shift[0];
+#pragma unroll
+                for (int j = 1; j < kW; j++) sh = i >= start[j] ? shift[j] : sh;
+                v[u] = i < total ? run[i + sh] : kSentinel;
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                if (v[u] == kSentinel) continue;
+                const int tx = (int)((v[u] >> 10) & (kTileTexels - 1));
+                const uint4 cc = col[v[u] & 1023];
+                atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
+                if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
+                if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
+        const int texel = t * kTileTexels + i;
+        if (texel >= num_texels) break;
+        const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
+        unsigned long long *qq = lm + 4 * (size_t)texel;
+        if (r) atomicAdd(qq + 0, r);
+        if (gg) atomicAdd(qq + 1, gg);
+        if (bb) atomicAdd(qq + 2, bb);
+    }
+}
+
 } // namespace
 
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s) {
     const int P = (num_texels + kTileTexels - 1) / kTileTexels;
+    const size_t plds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16;
+    if (sb.presort) {
+        hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre, (int)plds);
+        if (e != hipSuccess) return e;
+        const int G = (sb.groups + 7) & ~7;
+        hipLaunchKernelGGL(k_tile_runs_pre, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
+                           sb.stream, sb.toff, sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
+        return hipGetLastError();
+    }
     const uint64_t nslices = (sb.cap + kSlice - 1) / kSlice;
     hipLaunchKernelGGL(k_slice_sort, dim3((unsigned)nslices), dim3(256), 0, s, sb.stream, sb.cursor, sb.cap, P,
                        sb.sorted, sb.toff);

@@ -614,25 +614,29 @@ static uint64_t stream_cap_for(uint64_t items, int grid, int block) {
     return items * FMGI_EVENTS_PER_ITEM + (waves + 1) * FMGI_STREAM_BLOCK;
 }
 
-static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block) {
-    return stream_cap_for(items, grid, block) > c->sb_cap_alloc[k];
+static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block,
+                                       bool presort) {
+    return stream_cap_for(items, grid, block) > c->sb_cap_alloc[k] || (!presort && !c->sb[k].sorted);
 }
 
-static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block) {
+static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block, bool presort) {
     StreamBufs &sb = c->sb[k];
     const uint64_t cap = stream_cap_for(items, grid, block);
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
-    const uint64_t nslices = (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
+    /* run tables: per 8192-code slice (sorted by k_slice_sort), or per ring-sized segment (presorted) */
+    const uint64_t nslices = presort ? (cap + FMGI_RING_CODES - 1) / FMGI_RING_CODES
+                                     : (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
     const uint64_t entries = (uint64_t)(P + 1) * nslices;
-    if (cap > c->sb_cap_alloc[k]) {
+    if (cap > c->sb_cap_alloc[k] || (!presort && !sb.sorted)) {
         hipFree(sb.stream);
         hipFree(sb.sorted);
         sb.stream = sb.sorted = nullptr;
         c->sb_cap_alloc[k] = 0;
         HIPCHK(hipMalloc(&sb.stream, cap * sizeof(uint32_t)));
-        HIPCHK(hipMalloc(&sb.sorted, cap * sizeof(uint32_t)));
+        if (!presort) HIPCHK(hipMalloc(&sb.sorted, cap * sizeof(uint32_t))); /* presorted: no second copy */
         c->sb_cap_alloc[k] = cap;
     }
+    sb.presort = presort ? 1 : 0;
     if (entries > c->sb_entries_alloc[k]) {
         hipFree(sb.toff);
         sb.toff = nullptr;
@@ -956,11 +960,13 @@ static hipError_t time_end(fmgi_context *c, hipStream_t s, hipEvent_t t0, hipEve
 
 /* work items per STREAM chunk: codes for 800 deposits per item, twice (stream + sorted), for each of the
    `sets` buffer sets in use, in at most half of the device memory that is free or already held by them */
-static uint64_t stream_chunk_items(fmgi_context *c, int sets) {
+static uint64_t stream_chunk_items(fmgi_context *c, int sets, bool presort) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
-    const double avail = (double)fr + 8.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]);
-    uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * 2.0 * 4.0 * FMGI_EVENTS_PER_ITEM));
+    const double copies = presort ? 1.0 : 2.0; /* the stream, and the slice-sorted copy unless presorted */
+    const double held = 4.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]) * (c->sb[0].sorted ? 2.0 : 1.0);
+    const double avail = (double)fr + held;
+    uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * copies * 4.0 * FMGI_EVENTS_PER_ITEM));
     /* slices are indexed in 32 bits by the sort kernel's grid */
     const uint64_t max_items = ((1ull << 31) - 1) / FMGI_EVENTS_PER_ITEM * FMGI_STREAM_SLICE;
     items = std::min(items, max_items);
@@ -1077,7 +1083,12 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int lanes = grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block;
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
-    uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1);
+    /* presorted stream (bake-side counting sort by fold tile, no k_slice_sort pass): when the tiles fit
+       one histogram entry per lane (FMGI_PRESORT=0 turns it off) */
+    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
+    const char *pre_env = getenv("FMGI_PRESORT");
+    const bool presort = P >= 1 && P <= FMGI_PRESORT_MAX_TILES && !(pre_env && atoi(pre_env) == 0);
+    uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, presort);
     if (const char *ce = getenv("FMGI_CHUNK_ITEMS")) /* tests: force several chunks */
         if (atoll(ce) > 0) chunk = std::min<uint64_t>(chunk, (uint64_t)atoll(ce));
     if (pipeline > 1) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>((n + pipeline - 1) / pipeline, 4 * (uint64_t)lanes));
@@ -1099,11 +1110,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));
-        if (ensure_stream_needs_growth(c, k, ce - cb, grid, block)) { /* no fold may still read it */
+        if (ensure_stream_needs_growth(c, k, ce - cb, grid, block, presort)) { /* no fold may still read it */
             HIPCHK(hipStreamSynchronize(s));
             if (c->fold_stream) HIPCHK(hipStreamSynchronize(c->fold_stream));
         }
-        int rc = ensure_stream(c, k, ce - cb, grid, block);
+        int rc = ensure_stream(c, k, ce - cb, grid, block, presort);
         if (rc != FMGI_OK) return rc;
         StreamBufs &sb = c->sb[k];
         a.item_begin = cb;
@@ -1111,6 +1122,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.stream = sb.stream;
         a.stream_cap = sb.cap;
         a.stream_cursor = sb.cursor;
+        a.presort = presort ? 1 : 0;
+        a.ntiles = P;
+        a.toff = sb.toff;
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;

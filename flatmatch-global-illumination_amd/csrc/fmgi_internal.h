@@ -91,6 +91,11 @@ struct BakeArgs {
     uint64_t stream_cap;
     unsigned long long *stream_cursor;
     unsigned long long *overflow; /* set if a reservation would pass stream_cap (never, by sizing) */
+    /* presorted stream (P <= FMGI_PRESORT_MAX_TILES tiles): each wave writes its rings of
+       FMGI_RING_CODES codes sorted by fold tile, with the P + 1 run offsets of every ring-sized segment
+       in toff[segment * (P + 1) + t]; the fold then needs no sort pass */
+    int presort, ntiles;
+    uint16_t *toff;
     int ring_off;                 /* byte offset of the per-wave code rings in dynamic LDS (fmgi_bake_lds) */
     int num_texels;
     /* debug trace (TRACE kernels only) */
@@ -107,6 +112,8 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 #define FMGI_RING_CODES 1024   /* codes a wave collects in LDS before writing them out       */
 static_assert(FMGI_STREAM_BLOCK % FMGI_RING_CODES == 0, "ring flushes must tile the stream blocks");
 #define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
+#define FMGI_RING_STRIDE (FMGI_RING_CODES + 128) /* per-wave LDS: ring, its overflow (64), tile histogram (64) */
+#define FMGI_PRESORT_MAX_TILES 63 /* presorted stream: a tile histogram of one entry per lane        */
 #define FMGI_TILE_BITS 11      /* 2048-texel tiles summed in LDS (64 KB: two sum workgroups per
                                   CU; measured 25 ms per 1e9 photons vs 28 ms with 4096, 31 ms with 1024) */
 #define FMGI_MAX_TILES 2048    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */
@@ -120,6 +127,8 @@ struct StreamBufs {
     const uint32_t *colpack;    /* colour table {R, G - R, B - R, 0} per state (fixed point, the
                                    differences two's complement)                                */
     int groups;                 /* slice groups per tile in the sum kernel                      */
+    int presort;                /* codes were written presorted per FMGI_RING_CODES segment (toff per
+                                   segment); the fold skips k_slice_sort                         */
     int block;                  /* threads per sum workgroup (256, 512 or 1024)                  */
 };
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);

@@ -798,6 +798,87 @@ struct AccStream {
         ws.base += n;
     }
 
+    /* presorted stream: write ring[0, n) (n <= FMGI_RING_CODES) to the next FMGI_RING_CODES-code segment of
+       the block sorted by fold tile (counting sort in the wave's LDS histogram), and the segment's P + 1
+       run offsets to toff. Called where every live lane of the wave is active. */
+    static __device__ __forceinline__ void sorted_out(const BakeArgs &a, WaveStream &ws, uint32_t *ring,
+                                                      uint32_t n) {
+        if (ws.end - ws.base < FMGI_RING_CODES) reserve(a, ws);
+        if (ws.end - ws.base < FMGI_RING_CODES) return; /* overflow (counted in reserve) */
+        uint32_t *hist = (uint32_t *)ring + FMGI_RING_CODES + 64;
+        const uint64_t live = __ballot(true);
+        const uint32_t nl = (uint32_t)__popcll(live);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+        const int P = a.ntiles;
+        const uint32_t shift = 10 + FMGI_TILE_BITS;
+        for (uint32_t k = r; k < 64; k += nl) hist[k] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        const bool full = nl == 64 && n == FMGI_RING_CODES; /* every lane owns 16 consecutive codes */
+        uint32_t cr[16]; /* full: the lane's codes, held while the ring is overwritten in sorted order */
+        if (full) {
+            const uint4 *rq = (const uint4 *)ring + 4 * r;
+#pragma unroll
+            for (int h = 0; h < 4; h++) {
+                const uint4 c = rq[h];
+                cr[4 * h] = c.x, cr[4 * h + 1] = c.y, cr[4 * h + 2] = c.z, cr[4 * h + 3] = c.w;
+            }
+#pragma unroll
+            for (int e = 0; e < 16; e++) atomicAdd(&hist[cr[e] >> shift], 1u);
+        } else {
+            for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint16_t *to = a.toff + (ws.base / FMGI_RING_CODES) * (uint64_t)(P + 1);
+        if (nl == 64) { /* exclusive scan of the P counts, one per lane */
+            const uint32_t lane = r;
+            const uint32_t v = (int)lane < P ? hist[lane] : 0u;
+            uint32_t incl = v;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = __shfl_up(incl, off, 64);
+                if ((int)lane >= off) incl += o;
+            }
+            if ((int)lane < P) {
+                hist[lane] = incl - v;
+                to[lane] = (uint16_t)(incl - v);
+            }
+            if ((int)lane == P) to[P] = (uint16_t)n;
+        } else if (r == 0) { /* the tail of the bake, some lanes done: one lane scans */
+            uint32_t run = 0;
+            for (int t = 0; t < P; t++) {
+                const uint32_t c = hist[t];
+                hist[t] = run;
+                to[t] = (uint16_t)run;
+                run += c;
+            }
+            to[P] = (uint16_t)n;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        uint32_t *dst = a.stream + ws.base;
+        if (full) { /* scatter into the ring itself (LDS), then one coalesced copy to the segment */
+#pragma unroll
+            for (int h = 0; h < 16; h += 8) {
+                uint32_t o[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++) o[e] = atomicAdd(&hist[cr[h + e] >> shift], 1u);
+#pragma unroll
+                for (int e = 0; e < 8; e++) ring[o[e]] = cr[h + e];
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int h = 0; h < 4; h++) ((uint4 *)dst)[r + 64 * h] = ((const uint4 *)ring)[r + 64 * h];
+        } else {
+            for (uint32_t k = r; k < n; k += nl) {
+                const uint32_t c = ring[k];
+                dst[atomicAdd(&hist[c >> shift], 1u)] = c;
+            }
+        }
+        ws.base += FMGI_RING_CODES;
+    }
+
     static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, uint32_t *ring, bool dep,
                                                   uint32_t code) {
         const uint64_t m = __ballot(dep);
@@ -809,7 +890,8 @@ struct AccStream {
         ws.tot += n;
         if (fill + n < FMGI_RING_CODES) return;
         /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
-        copy_out(a, ws, ring, FMGI_RING_CODES);
+        if (a.presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
+        else copy_out(a, ws, ring, FMGI_RING_CODES);
         const uint32_t rest = fill + n - FMGI_RING_CODES; /* < n <= live lanes: one code per live lane */
         const uint64_t live = __ballot(true);
         const uint32_t k = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
@@ -832,6 +914,13 @@ struct AccStream {
         ws.end = __shfl(ws.end, src, 64);
         const uint32_t fill = ws.tot % FMGI_RING_CODES, padded = (fill + 3) & ~3u;
         const uint32_t lane = __lane_id();
+        if (a.presort) { /* the last (partial) ring, then empty run tables for the block's unused segments */
+            if (fill) sorted_out(a, ws, ring, fill);
+            const int P = a.ntiles;
+            for (uint64_t sg = ws.base / FMGI_RING_CODES; sg < ws.end / FMGI_RING_CODES; sg++)
+                for (int t = (int)lane; t <= P; t += 64) a.toff[sg * (uint64_t)(P + 1) + t] = 0;
+            return;
+        }
         for (uint32_t k = fill + lane; k < padded; k += 64) ring[k] = 0xFFFFFFFFu;
         if (padded) copy_out(a, ws, ring, padded);
         for (uint64_t k = ws.base + lane; k < ws.end; k += 64) a.stream[k] = 0xFFFFFFFFu;
@@ -887,7 +976,7 @@ template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
     /* AccStream: this wave's ring of deposit codes, after the scan image in LDS */
-    uint32_t *const ring = (uint32_t *)(s_img + a.ring_off) + (threadIdx.x >> 6) * (FMGI_RING_CODES + 64);
+    uint32_t *const ring = (uint32_t *)(s_img + a.ring_off) + (threadIdx.x >> 6) * FMGI_RING_STRIDE;
     if (Scan::kLds) { /* stage the filter image once per workgroup */
         const int n16 = a.fimg_bytes >> 4;
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
@@ -1252,7 +1341,7 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
-    return img + (accum == 4 ? (size_t)(block / 64) * (FMGI_RING_CODES + 64) * 4 : 0);
+    return img + (accum == 4 ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
 
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes) {

@@ -152,6 +152,25 @@ def test_lightmap_box_prefix_exact(torch_cuda, box200, box2000, offsets, kernel,
         ctx.close()
 
 
+@pytest.mark.parametrize("presort", ["1", "0"])
+def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, presort):
+    """The STREAM fold from the bake-side presorted segments (FMGI_PRESORT=1, the default for lightmaps of
+    at most 63 fold tiles) and from the slice-sorted stream (FMGI_PRESORT=0) give the oracle's lightmap,
+    for full-ring flushes and for the partial rings at the end of a launch."""
+    os.environ["FMGI_PRESORT"] = presort
+    try:
+        for sc, spa, lo, hi in ((box200, 172_413_793, 7_000, 27_000), (example_scene, 65_000, 0, 300)):
+            L = _oracle_plan(sc, spa, offsets)
+            ctx = _ctx(sc, spa, offsets, fmgi.ACCUM_STREAM)
+            lm = _bake_gpu(torch_cuda, ctx, lo, hi, fmgi.KERNEL_AUTO)
+            olm, _ = O.bake(sc, L, lo, hi)
+            assert np.array_equal(lm[:, :3], olm), sc.name
+            assert ctx.stats()["stream_overflow"] == 0
+            ctx.close()
+    finally:
+        os.environ.pop("FMGI_PRESORT", None)
+
+
 def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets):
     """Config 3 sized work (a 1e8-photon slice): order-free exact accumulation means any split of the
     item range, and any repetition, gives identical bits."""
@@ -173,6 +192,11 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     finally:
         os.environ.pop("FMGI_CHUNK_ITEMS", None)
         os.environ.pop("FMGI_PIPELINE", None)
+    os.environ["FMGI_PRESORT"] = "0"  # the slice-sorted fold (lightmaps of more than 63 fold tiles)
+    try:
+        g = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+    finally:
+        os.environ.pop("FMGI_PRESORT", None)
     d1 = _bake_gpu(torch_cuda, ctx, 0, 12_345, fmgi.KERNEL_GRID)
     d2 = _bake_gpu(torch_cuda, ctx, 12_345, n, fmgi.KERNEL_GRID)
     assert np.array_equal(a, b1 + b2)
@@ -180,6 +204,7 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     assert np.array_equal(a, d)
     assert np.array_equal(a, e)
     assert np.array_equal(a, f)
+    assert np.array_equal(a, g)
     assert np.array_equal(a, d1 + d2)
     assert ctx.stats()["stream_overflow"] == 0
     ctx.reset_stats()
