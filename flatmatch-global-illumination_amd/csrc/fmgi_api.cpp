@@ -647,13 +647,14 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     if (!sb.cursor) HIPCHK(hipMalloc(&sb.cursor, 64));
     sb.cap = cap;
     sb.colpack = c->d_colpack;
-    /* k_tile_runs runs one 112-KiB workgroup per CU at a time and tiles carry uneven code counts:
-       ~8 rounds of P x groups workgroups balance the tail (box200, 23 tiles: 28.4 ms fold at 89
-       groups vs 31.1 ms at 23 and 34.8 ms at 11; flat from ~33 groups up) */
+    /* the fold kernels run two 64-KiB workgroups per CU and tiles carry uneven code counts: ~8 (slice-
+       sorted) or ~16 (presorted) rounds of P x groups workgroups balance the tail (box200, 46 tiles,
+       presorted: 19.6 / 18.9 / 17.4 / 16.5 ms at 11 / 22 / 45 / 90 groups) */
     {
         const int ncu = std::max(1, c->num_cus);
         const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
-        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (8 * ncu + P - 1) / P);
+        const int rounds = presort ? 16 : 8;
+        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
         const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
     }

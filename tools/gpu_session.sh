@@ -12,6 +12,7 @@
 #   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
 #   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
 #   pmc              rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on a short bench ($PROF_ARGS)
+#   foldpmc          one rocprofv3 --pmc pass of LDS-pipe counters (the fold kernels' binding resource)
 #   sq               two rocprofv3 --pmc passes of SQ instruction / wait counters ($PROF_ARGS)
 # Each GPU step has its own time limit; a crash/timeout (rc > 1) stops the session.
 set -u
@@ -45,6 +46,7 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     pmclist) step pmclist 120 rocprofv3 -L ;;
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU -d "$OUT/sq1" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step sq2 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_BRANCH -d "$OUT/sq2" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    foldpmc) step fold_lds 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS -d "$OUT/fold_lds" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
   esac
