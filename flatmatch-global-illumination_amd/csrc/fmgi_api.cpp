@@ -655,6 +655,10 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
         const int rounds = presort ? 16 : 8;
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
+        /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
+           without a segment group: at least 256 segments (16 per wave) per workgroup */
+        if (presort && !(ge && atoi(ge) > 0))
+            sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 256));
         const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
     }
@@ -982,10 +986,20 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
                                                   (unsigned long long)b, (unsigned long long)e,
                                                   (unsigned long long)c->total_items);
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_HYBRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
-    if (kernel == FMGI_KERNEL_AUTO) kernel = c->auto_kernel;
+    const bool was_auto = kernel == FMGI_KERNEL_AUTO;
+    if (was_auto) kernel = c->auto_kernel;
     const int block = bake_block();
     kernel = fitting_kernel(c, kernel, c->accum, block); /* an image too large for LDS: same results, other scan */
     if (b == e) return FMGI_OK;
+    /* a launch with at most half as many items as resident lanes runs ScanFast with cooperative lanes
+       (below): on such launches that beats the hybrid scan's single lane per item (config 1: 6.6 ms
+       hybrid bake vs ~3.5 ms cooperative) */
+    if (was_auto && kernel == FMGI_KERNEL_HYBRID && !trace && c->accum == FMGI_ACCUM_STREAM &&
+        fitting_kernel(c, FMGI_KERNEL_FAST, c->accum, block) == FMGI_KERNEL_FAST) {
+        const uint64_t lanes_max =
+            (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, c->accum, trace, block, UINT64_MAX) * block;
+        if ((e - b) * 2 <= lanes_max) kernel = FMGI_KERNEL_FAST;
+    }
     if (c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     /* no walls: every photon escapes at its first scan (photonmap.cl:208), so nothing is deposited */
     if (c->nrects == 0) return FMGI_OK;
