@@ -656,9 +656,10 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         const int rounds = presort ? 16 : 8;
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
-           without a segment group: at least 256 segments (16 per wave) per workgroup */
+           without a segment group, and each pays its LDS set-up and tile flush: at least 1024 segments
+           (64 per wave) per workgroup */
         if (presort && !(ge && atoi(ge) > 0))
-            sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 256));
+            sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 1024));
         const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
     }
@@ -1426,7 +1427,14 @@ static void dropin_release_shard(DropinShard &S) {
     S = DropinShard{};
 }
 
+/* the host-only context that plans the reference schedule (its scene set once per geometry) */
+static fmgi_context *g_plan_ctx = nullptr;
+static uint64_t g_plan_hash = 0;
+
 static void dropin_release_locked() {
+    fmgi_destroy(g_plan_ctx);
+    g_plan_ctx = nullptr;
+    g_plan_hash = 0;
     for (DropinShard &S : g_dropin) dropin_release_shard(S);
     g_dropin.clear();
     if (g_dropin_tex && hipSetDevice(g_dropin_tex_dev) == hipSuccess) (void)hipFree(g_dropin_tex);
@@ -1530,22 +1538,31 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     std::vector<int32_t> offs;
     uint64_t items = 0;
     int64_t nl = 0;
-    {
-        fmgi_context *h = fmgi_create(FMGI_HOST_ONLY);
-        int rc0 = fmgi_set_scene(h, geo->walls, geo->numWalls, geo->windows, geo->numWindows, geo->lights,
-                                 geo->numLights, geo->numTexels);
-        if (rc0 == FMGI_OK) nl = fmgi_plan(h, spa, wg, nullptr, 0, &items);
-        if (rc0 == FMGI_OK && nl >= 0)
-            for (const LaunchDev &L : h->h_launches) offs.push_back(L.rng_offset);
-        fmgi_destroy(h);
-        if (rc0 != FMGI_OK) return rc0;
+    std::lock_guard<std::mutex> lk(g_dropin_mu);
+    {   /* the planning context and its scene are kept across calls per geometry, like the shards' */
+        const uint64_t hash = geometry_hash(geo);
+        if (!g_plan_ctx || g_plan_hash != hash) {
+            fmgi_destroy(g_plan_ctx);
+            g_plan_hash = 0;
+            g_plan_ctx = fmgi_create(FMGI_HOST_ONLY);
+            if (!g_plan_ctx) return set_err(FMGI_ERR_OOM, "planning context");
+            const int rc0 = fmgi_set_scene(g_plan_ctx, geo->walls, geo->numWalls, geo->windows, geo->numWindows,
+                                           geo->lights, geo->numLights, geo->numTexels);
+            if (rc0 != FMGI_OK) {
+                fmgi_destroy(g_plan_ctx);
+                g_plan_ctx = nullptr;
+                return rc0;
+            }
+            g_plan_hash = hash;
+        }
+        nl = fmgi_plan(g_plan_ctx, spa, wg, nullptr, 0, &items);
         if (nl < 0) return (int)nl;
+        for (const LaunchDev &L : g_plan_ctx->h_launches) offs.push_back(L.rng_offset);
     }
     RandGuard guard;
     guard.save();
     int rc_all;
     {
-        std::lock_guard<std::mutex> lk(g_dropin_mu);
         rc_all = bake_geometry_devices(geo, spa, wg, kernel, offs, items, texels_out, verbose);
         const char *ce = getenv("FMGI_DROPIN_CACHE");
         if (rc_all != FMGI_OK || (ce && atoi(ce) == 0)) dropin_release_locked();
