@@ -461,6 +461,18 @@ struct fmgi_context {
     uint64_t sb_entries_alloc[2] = {0, 0};
     hipStream_t fold_stream = nullptr;
     hipEvent_t ev_baked[2] = {nullptr, nullptr}, ev_folded[2] = {nullptr, nullptr};
+    /* fetch order (bake_common): per-source item ranges of the plan, scans per item measured on the
+       previous bake (device totals -> pinned host copy, ready when ev_cost has completed) */
+    std::vector<uint64_t> src_lo, src_hi;
+    std::vector<double> src_cost_per_item;
+    unsigned long long *d_src_cost = nullptr, *h_src_cost = nullptr;
+    int src_cost_n = 0;
+    hipEvent_t ev_cost = nullptr;
+    bool cost_pending = false;
+    uint64_t *d_fetch_tab = nullptr;
+    int fetch_tab_cap = 0;
+    std::vector<std::vector<uint64_t>> h_fetch_tab; /* the host side of each launch's table, kept for the call */
+    std::vector<uint64_t> cost_items;               /* items per source of the measured call */
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -535,6 +547,10 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     for (auto &p : c->ev_fold) { hipEventDestroy(p.first); hipEventDestroy(p.second); }
     hipFree(c->d_src_item_begin);
     hipFree(c->d_src_launch0);
+    if (c->ev_cost) { hipEventSynchronize(c->ev_cost); hipEventDestroy(c->ev_cost); }
+    hipFree(c->d_src_cost);
+    if (c->h_src_cost) hipHostFree(c->h_src_cost);
+    hipFree(c->d_fetch_tab);
     hipFree(c->d_counts);
     hipFree(c->d_colfx);
     if (c->fold_stream) hipStreamSynchronize(c->fold_stream);
@@ -909,6 +925,17 @@ FMGI_API int64_t fmgi_plan(fmgi_context *c, int spa, int wg, const int32_t *rng_
     HIPCHK(hipMemcpy(c->d_src_item_begin, sib.data(), sib.size() * sizeof(uint64_t), hipMemcpyHostToDevice));
     HIPCHK(hipMemcpy(c->d_src_launch0, sl0.data(), sl0.size() * sizeof(int32_t), hipMemcpyHostToDevice));
     }
+    {   /* per-source item ranges (a source's launches are consecutive in the schedule) */
+        const bool same = (int)c->src_lo.size() == c->nsrcs;
+        std::vector<uint64_t> lo((size_t)c->nsrcs, UINT64_MAX), hi((size_t)c->nsrcs, 0);
+        for (const LaunchDev &l : L) {
+            lo[(size_t)l.source] = std::min<uint64_t>(lo[(size_t)l.source], l.item_begin);
+            hi[(size_t)l.source] = std::max<uint64_t>(hi[(size_t)l.source], l.item_begin + l.count);
+        }
+        if (!same || lo != c->src_lo || hi != c->src_hi) c->src_cost_per_item.clear(); /* other schedule */
+        c->src_lo.swap(lo);
+        c->src_hi.swap(hi);
+    }
     c->launch_cap = (uint32_t)cap;
     c->h_launches.swap(L);
     c->total_items = item;
@@ -1076,7 +1103,98 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         }
         if (a.coop > 1) kernel = FMGI_KERNEL_FAST_COOP;
     }
+    /* fetch order: the lanes fetch work items through a table of source ranges, the sources whose items
+       took the most scans on this context's previous bake first (longest-processing-time first), so
+       the end of a launch with few items per lane is not a run of the longest items (example.png, config
+       2, 3 items per lane: the last sources' items are the longest). The lightmap is an order-free exact
+       sum, so any order gives the same bits. The first bake of a schedule measures (one atomic per item
+       into a per-source total); FMGI_FETCH_ORDER=0 turns it off. */
+    constexpr int kMaxTabs = 64;
+    const char *fo_env = getenv("FMGI_FETCH_ORDER");
+    const bool order_on = !(fo_env && atoi(fo_env) == 0) && c->nsrcs > 0;
+    const int ns = c->nsrcs;
+    if (order_on) {
+        if (!c->ev_cost) HIPCHK(hipEventCreateWithFlags(&c->ev_cost, hipEventDisableTiming));
+        if (c->cost_pending && hipEventQuery(c->ev_cost) == hipSuccess) { /* the previous measurement */
+            c->cost_pending = false;
+            if (c->src_cost_per_item.size() != (size_t)ns) c->src_cost_per_item.assign((size_t)ns, 0.0);
+            for (int k = 0; k < ns && k < (int)c->cost_items.size(); k++)
+                if (c->cost_items[(size_t)k]) c->src_cost_per_item[(size_t)k] = (double)c->h_src_cost[k] / (double)c->cost_items[(size_t)k];
+        }
+        /* the previous call's kernels (maybe on another stream) are done with the table and the totals */
+        HIPCHK(hipStreamWaitEvent(s, c->ev_cost, 0));
+        if (c->fetch_tab_cap < kMaxTabs * 2 * ns) {
+            hipFree(c->d_fetch_tab);
+            c->d_fetch_tab = nullptr;
+            c->fetch_tab_cap = 0;
+            HIPCHK(hipMalloc(&c->d_fetch_tab, (size_t)kMaxTabs * 2 * ns * sizeof(uint64_t)));
+            c->fetch_tab_cap = kMaxTabs * 2 * ns;
+        }
+        if (!c->cost_pending && c->src_cost_per_item.empty()) { /* measure: the first bake of a schedule */
+            if (c->src_cost_n < ns) {
+                hipFree(c->d_src_cost);
+                if (c->h_src_cost) (void)hipHostFree(c->h_src_cost);
+                c->d_src_cost = c->h_src_cost = nullptr;
+                c->src_cost_n = 0;
+                HIPCHK(hipMalloc(&c->d_src_cost, (size_t)ns * 8));
+                HIPCHK(hipHostMalloc((void **)&c->h_src_cost, (size_t)ns * 8, hipHostMallocDefault));
+                c->src_cost_n = ns;
+            }
+            HIPCHK(hipMemsetAsync(c->d_src_cost, 0, (size_t)ns * 8, s));
+            a.src_cost = c->d_src_cost;
+            c->cost_items.assign((size_t)ns, 0);
+            for (int k = 0; k < ns && k < (int)c->src_lo.size(); k++) {
+                const uint64_t lo = std::max(c->src_lo[(size_t)k], b), hi = std::min(c->src_hi[(size_t)k], e);
+                c->cost_items[(size_t)k] = lo < hi ? hi - lo : 0;
+            }
+        }
+        c->h_fetch_tab.resize(kMaxTabs);
+    }
+    int ntab = 0;
+    /* only launches of at most 16 items per resident lane reorder (box200's 30 per lane: plain order) */
+    const uint64_t order_lanes =
+        order_on ? (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block / (uint64_t)a.coop : 0;
+    auto fetch_table = [&](uint64_t cb, uint64_t ce) -> hipError_t { /* a.fetch_tab for items [cb, ce) */
+        a.fetch_tab = nullptr;
+        a.fetch_nseg = 0;
+        if (!order_on || c->src_cost_per_item.size() != (size_t)ns || (int)c->src_lo.size() != ns || ntab >= kMaxTabs ||
+            ce - cb > 16 * order_lanes)
+            return hipSuccess;
+        std::vector<int> ord((size_t)ns);
+        for (int k = 0; k < ns; k++) ord[(size_t)k] = k;
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) {
+            return c->src_cost_per_item[(size_t)x] > c->src_cost_per_item[(size_t)y];
+        });
+        std::vector<uint64_t> &h = c->h_fetch_tab[(size_t)ntab];
+        h.clear();
+        uint64_t f = 0;
+        for (int k : ord) {
+            const uint64_t lo = std::max(c->src_lo[(size_t)k], cb), hi = std::min(c->src_hi[(size_t)k], ce);
+            if (lo >= hi) continue;
+            h.push_back(f);
+            h.push_back(lo);
+            f += hi - lo;
+        }
+        if (f != ce - cb || h.empty()) return hipSuccess; /* not covered: plain order */
+        uint64_t *d = c->d_fetch_tab + (size_t)ntab * 2 * ns;
+        hipError_t err = hipMemcpyAsync(d, h.data(), h.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        if (err != hipSuccess) return err;
+        a.fetch_tab = d;
+        a.fetch_nseg = (int)(h.size() / 2);
+        ntab++;
+        return hipSuccess;
+    };
+    auto finish_call = [&]() -> hipError_t { /* the measured totals to the host, and the call's end marker */
+        if (!order_on) return hipSuccess;
+        if (a.src_cost) {
+            hipError_t err = hipMemcpyAsync(c->h_src_cost, c->d_src_cost, (size_t)ns * 8, hipMemcpyDeviceToHost, s);
+            if (err != hipSuccess) return err;
+            c->cost_pending = true;
+        }
+        return hipEventRecord(c->ev_cost, s);
+    };
     if (c->accum != FMGI_ACCUM_STREAM) {
+        HIPCHK(fetch_table(b, e));
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
@@ -1086,6 +1204,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
         if (a.counts)
             HIPCHK(fmgi_launch_reduce_states(a.counts, c->d_colfx, (unsigned long long *)lm, c->num_texels, s));
+        HIPCHK(finish_call());
         return FMGI_OK;
     }
     /* STREAM: the codes of a chunk of work items are held in HBM (2 x 4 B per deposit, worst case 800
@@ -1141,6 +1260,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.presort = presort ? 1 : 0;
         a.ntiles = P;
         a.toff = sb.toff;
+        HIPCHK(fetch_table(cb, ce));
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
@@ -1159,6 +1279,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (overlap) { /* everything after this call on s sees the complete lightmap */
         HIPCHK(hipStreamWaitEvent(s, c->ev_folded[(nchunk - 1) & 1], 0));
     }
+    HIPCHK(finish_call());
     return FMGI_OK;
 }
 

@@ -80,6 +80,10 @@ struct BakeArgs {
     int grid_xy_separate; /* layouts: walk the x and y planes one axis after the other (else merged) */
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
+    const uint64_t *fetch_tab;    /* fetch_nseg > 0: [f_begin, item_begin] pairs, f_begin ascending from 0:
+                                     fetch f maps into the segment holding it (sums are order-free) */
+    int fetch_nseg;
+    unsigned long long *src_cost; /* non-null: per-source scan totals of the finished items */
     int grid_code_or;     /* ScanHybrid: flag or-ed into the codes of grid records (rect indices)    */
     int coop;             /* lanes per work item (1, 2, 4, 8; ScanFast only): small launches split each
                              scan's records over several lanes instead of leaving the GPU mostly idle */

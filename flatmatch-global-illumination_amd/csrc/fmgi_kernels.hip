@@ -991,7 +991,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     int nev = 0;
     /* per-lane counts of one launch, in 32 bits: a lane traces a few dozen work items per launch (the
        grid is occupancy-sized, chunks are memory-sized); scans = deposits + escapes */
-    uint32_t n_ph = 0, n_dep = 0, n_esc = 0;
+    uint32_t n_ph = 0, n_dep = 0, n_esc = 0, scan0 = 0;
     ScanStats sst;
     WaveStream ws;
     /* BakeArgs::coop lanes per work item (ScanFast splits each scan's records among them; they keep
@@ -1008,6 +1008,10 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                     a.ev_counts[item - a.item_begin] = nev;
                     a.rng_final[item - a.item_begin] = rng;
                 }
+                /* the finished item's scans, per source: the host orders the next bake's fetches by it */
+                if (a.src_cost && lead && n_dep + n_esc != scan0)
+                    atomicAdd(a.src_cost + srci, (unsigned long long)(n_dep + n_esc - scan0));
+                scan0 = n_dep + n_esc;
                 if (sst.tests && lead) { /* flush this lane's rect-test count (see ScanStats) */
                     atomicAdd(a.stats + KSTAT_TESTS, (unsigned long long)sst.tests);
                 }
@@ -1015,8 +1019,17 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 /* one fetch per work item: by the group's lead lane, broadcast to its coop lanes */
                 uint64_t w = lead ? atomicAdd(a.counter, 1ull) : 0ull;
                 if (Scan::kCoop) w = __shfl(w, (int)__lane_id() & ~(a.coop - 1), 64);
-                w += a.item_begin;
-                if (w >= a.item_end) break;
+                if (w >= a.item_end - a.item_begin) break;
+                if (a.fetch_nseg > 0) { /* fetch order: segments of source ranges, costliest items first */
+                    int lo = 0, hi = a.fetch_nseg - 1;
+                    while (lo < hi) {
+                        const int mid = (lo + hi + 1) >> 1;
+                        if (a.fetch_tab[2 * mid] <= w) lo = mid; else hi = mid - 1;
+                    }
+                    w = a.fetch_tab[2 * lo + 1] + (w - a.fetch_tab[2 * lo]);
+                } else {
+                    w += a.item_begin;
+                }
                 item = w;
                 int li;
                 uint32_t gid;
