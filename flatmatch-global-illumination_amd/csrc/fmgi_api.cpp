@@ -469,9 +469,9 @@ struct fmgi_context {
     int src_cost_n = 0;
     hipEvent_t ev_cost = nullptr;
     bool cost_pending = false;
-    uint64_t *d_fetch_tab = nullptr;
+    uint32_t *d_fetch_tab = nullptr;
     int fetch_tab_cap = 0;
-    std::vector<std::vector<uint64_t>> h_fetch_tab; /* the host side of each launch's table, kept for the call */
+    std::vector<std::vector<uint32_t>> h_fetch_tab; /* the host side of each launch's table, kept for the call */
     std::vector<uint64_t> cost_items;               /* items per source of the measured call */
 };
 
@@ -1127,7 +1127,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             hipFree(c->d_fetch_tab);
             c->d_fetch_tab = nullptr;
             c->fetch_tab_cap = 0;
-            HIPCHK(hipMalloc(&c->d_fetch_tab, (size_t)kMaxTabs * 2 * ns * sizeof(uint64_t)));
+            HIPCHK(hipMalloc(&c->d_fetch_tab, (size_t)kMaxTabs * 2 * ns * sizeof(uint32_t)));
             c->fetch_tab_cap = kMaxTabs * 2 * ns;
         }
         if (!c->cost_pending && c->src_cost_per_item.empty()) { /* measure: the first bake of a schedule */
@@ -1158,26 +1158,26 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.fetch_tab = nullptr;
         a.fetch_nseg = 0;
         if (!order_on || c->src_cost_per_item.size() != (size_t)ns || (int)c->src_lo.size() != ns || ntab >= kMaxTabs ||
-            ce - cb > 16 * order_lanes)
+            ce - cb > 16 * order_lanes || ce > 0xFFFFFFFFull)
             return hipSuccess;
         std::vector<int> ord((size_t)ns);
         for (int k = 0; k < ns; k++) ord[(size_t)k] = k;
         std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) {
             return c->src_cost_per_item[(size_t)x] > c->src_cost_per_item[(size_t)y];
         });
-        std::vector<uint64_t> &h = c->h_fetch_tab[(size_t)ntab];
+        std::vector<uint32_t> &h = c->h_fetch_tab[(size_t)ntab];
         h.clear();
         uint64_t f = 0;
         for (int k : ord) {
             const uint64_t lo = std::max(c->src_lo[(size_t)k], cb), hi = std::min(c->src_hi[(size_t)k], ce);
             if (lo >= hi) continue;
-            h.push_back(f);
-            h.push_back(lo);
+            h.push_back((uint32_t)f);
+            h.push_back((uint32_t)lo);
             f += hi - lo;
         }
         if (f != ce - cb || h.empty()) return hipSuccess; /* not covered: plain order */
-        uint64_t *d = c->d_fetch_tab + (size_t)ntab * 2 * ns;
-        hipError_t err = hipMemcpyAsync(d, h.data(), h.size() * sizeof(uint64_t), hipMemcpyHostToDevice, s);
+        uint32_t *d = c->d_fetch_tab + (size_t)ntab * 2 * ns;
+        hipError_t err = hipMemcpyAsync(d, h.data(), h.size() * sizeof(uint32_t), hipMemcpyHostToDevice, s);
         if (err != hipSuccess) return err;
         a.fetch_tab = d;
         a.fetch_nseg = (int)(h.size() / 2);

@@ -80,7 +80,7 @@ struct BakeArgs {
     int grid_xy_separate; /* layouts: walk the x and y planes one axis after the other (else merged) */
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
-    const uint64_t *fetch_tab;    /* fetch_nseg > 0: [f_begin, item_begin] pairs, f_begin ascending from 0:
+    const uint32_t *fetch_tab;    /* fetch_nseg > 0: [f_begin, item_begin] pairs, f_begin ascending from 0:
                                      fetch f maps into the segment holding it (sums are order-free) */
     int fetch_nseg;
     unsigned long long *src_cost; /* non-null: per-source scan totals of the finished items */

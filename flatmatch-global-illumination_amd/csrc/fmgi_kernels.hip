@@ -150,6 +150,7 @@ struct ScanStats {
 struct ScanExact {
     static constexpr bool kLds = false;
     static constexpr bool kCoop = false;
+    static constexpr int kMinWaves = 1; /* k_bake occupancy floor for the register allocator */
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float best;
@@ -249,6 +250,7 @@ template <bool Coop>
 struct ScanFastT {
     static constexpr bool kLds = true;
     static constexpr bool kCoop = Coop;
+    static constexpr int kMinWaves = 1; /* k_bake occupancy floor for the register allocator */
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
@@ -579,6 +581,7 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
 struct ScanGrid {
     static constexpr bool kLds = true;
     static constexpr bool kCoop = false;
+    static constexpr int kMinWaves = 5; /* k_bake occupancy floor for the register allocator */
     static constexpr int kOrderedRounds = 12;
 
     /*
@@ -679,6 +682,7 @@ struct ScanGrid {
 struct ScanHybrid {
     static constexpr bool kLds = true;
     static constexpr bool kCoop = false;
+    static constexpr int kMinWaves = 1; /* k_bake occupancy floor for the register allocator */
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
@@ -969,8 +973,8 @@ __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
  */
 #ifdef FMGI_WAVES_PER_EU /* experiment builds: ask the register allocator for this occupancy */
 #define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(FMGI_WAVES_PER_EU)))
-#else
-#define FMGI_BAKE_ATTR
+#else /* ScanGrid: 5 waves/SIMD (96 VGPRs, no spills; unconstrained it takes 98 and 4 waves, -2.5 %) */
+#define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(Scan::kMinWaves)))
 #endif
 template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
@@ -991,7 +995,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     int nev = 0;
     /* per-lane counts of one launch, in 32 bits: a lane traces a few dozen work items per launch (the
        grid is occupancy-sized, chunks are memory-sized); scans = deposits + escapes */
-    uint32_t n_ph = 0, n_dep = 0, n_esc = 0, scan0 = 0;
+    uint32_t n_ph = 0, n_dep = 0, n_esc = 0;
     ScanStats sst;
     WaveStream ws;
     /* BakeArgs::coop lanes per work item (ScanFast splits each scan's records among them; they keep
@@ -1008,10 +1012,11 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                     a.ev_counts[item - a.item_begin] = nev;
                     a.rng_final[item - a.item_begin] = rng;
                 }
-                /* the finished item's scans, per source: the host orders the next bake's fetches by it */
-                if (a.src_cost && lead && n_dep + n_esc != scan0)
-                    atomicAdd(a.src_cost + srci, (unsigned long long)(n_dep + n_esc - scan0));
-                scan0 = n_dep + n_esc;
+                /* the finished item's scans, per source (the host orders the next bake's fetches by them):
+                   the lane's running scan count is added here and was subtracted at the item's fetch, so
+                   no register holds the item's start count */
+                if (a.src_cost && lead && photon >= 0)
+                    atomicAdd(a.src_cost + srci, (unsigned long long)(n_dep + n_esc));
                 if (sst.tests && lead) { /* flush this lane's rect-test count (see ScanStats) */
                     atomicAdd(a.stats + KSTAT_TESTS, (unsigned long long)sst.tests);
                 }
@@ -1020,13 +1025,15 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 uint64_t w = lead ? atomicAdd(a.counter, 1ull) : 0ull;
                 if (Scan::kCoop) w = __shfl(w, (int)__lane_id() & ~(a.coop - 1), 64);
                 if (w >= a.item_end - a.item_begin) break;
-                if (a.fetch_nseg > 0) { /* fetch order: segments of source ranges, costliest items first */
+                if (a.fetch_nseg > 0) { /* fetch order: segments of source ranges, costliest items first
+                                           (32-bit: the host builds a table only below 2^32 items) */
+                    const uint32_t f = (uint32_t)w;
                     int lo = 0, hi = a.fetch_nseg - 1;
                     while (lo < hi) {
                         const int mid = (lo + hi + 1) >> 1;
-                        if (a.fetch_tab[2 * mid] <= w) lo = mid; else hi = mid - 1;
+                        if (a.fetch_tab[2 * mid] <= f) lo = mid; else hi = mid - 1;
                     }
-                    w = a.fetch_tab[2 * lo + 1] + (w - a.fetch_tab[2 * lo]);
+                    w = a.fetch_tab[2 * lo + 1] + (f - a.fetch_tab[2 * lo]);
                 } else {
                     w += a.item_begin;
                 }
@@ -1034,6 +1041,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 int li;
                 uint32_t gid;
                 locate_item(a, w, srci, li, gid);
+                if (a.src_cost && lead) atomicAdd(a.src_cost + srci, 0ull - (unsigned long long)(n_dep + n_esc));
                 rng = gid + (uint32_t)a.launches[li].rng_offset; /* photonmap.cl:272 */
                 /* photonmap.cl:273-275: r = rand()*40; ceil(r) further draws, as one LCG jump */
                 const float r40 = rng_next(rng) * 40;
