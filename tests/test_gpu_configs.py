@@ -85,6 +85,10 @@ def test_config2_full_lightmap_exact(torch_cuda, example_scene, offsets):
     for k in ("photons", "scans", "deposits", "escapes"):
         assert st[k] == ost[k], k
     assert st["stream_overflow"] == 0
+    # the first bake measured scans per item per source; this one fetches the costliest sources first
+    # (3 items per lane: the reordered fetch table is in use) and must give the same bits
+    lm2 = _bake_gpu(torch_cuda, ctx, 0, n)
+    assert np.array_equal(lm2, lm)
     ctx.close()
 
 
