@@ -365,6 +365,13 @@ def main():
             tot = sum(cyc[k] for k in range(len(names))) or 1
             out["stage_cycles_frac"] = {n: cyc[k] / tot for k, n in enumerate(names)}
             out["note"] = "PROFILING BUILD (s_memtime per stage): value is not a valid bench number"
+        if os.environ.get("FMGI_LIB") == "clock":  # diagnostic build: s_memtime / s_memrealtime per wave
+            import ctypes as C
+
+            cyc = (C.c_uint64 * 16)()
+            ctx.lib.fmgi_get_stage_cycles(ctx.h, cyc)
+            out["in_kernel_clock_ghz"] = 0.1 * cyc[8] / max(cyc[9], 1)
+            out["note"] = "CLOCK BUILD (FMGI_CLOCK_STAMP): in-kernel clock of k_bake, median-free wave-time weighted"
         if world == 1 and not args.no_cpu_baseline:
             port = cpu_baseline(sc, cfg["spa"], args.cpu_seconds)
             ref = cpu_baseline_reference(sc, args.cpu_seconds)

@@ -73,6 +73,9 @@ __global__ __launch_bounds__(256) void k_slice_sort(const uint32_t *__restrict__
     for (int k = 0; k < per; k++) { /* all loads in flight before the first LDS atomic */
         const uint64_t i = b0 + (uint64_t)k * 256 + threadIdx.x;
         c[k] = i < n ? stream[i] : kSentinel;
+        /* a code of a tile >= P is never written by the bake; only the unwritten part of a block whose
+           reservation failed (stream overflow, reported by the call) can hold one: dropped */
+        if (c[k] != kSentinel && tile_of(c[k]) >= P) c[k] = kSentinel;
     }
 #pragma unroll
     for (int k = 0; k < per; k++)
@@ -186,8 +189,11 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
         r0 = 0, len = 0;
         if (lane < kW && s0 + lane < s_hi) {
             const uint16_t *to = toff + (s0 + lane) * (uint64_t)(P + 1);
-            r0 = to[t];
-            len = (int)to[t + 1] - r0;
+            /* clamped to the segment: a block whose reservation failed (stream overflow, never by sizing;
+               the call then reports the error) has no run table written, and its stale offsets must not
+               send a read past the segment */
+            r0 = min((int)to[t], FMGI_RING_CODES);
+            len = max(0, min((int)to[t + 1], FMGI_RING_CODES) - r0);
         }
     };
     int nr0, nlen;

@@ -13,7 +13,9 @@
  * same IEEE fp32 bits photonmap.cl computes on the device.
  */
 #include <hip/hip_runtime_api.h>
+#include <rccl/rccl.h>
 
+#include <dlfcn.h>
 #include <math.h>
 #include <stdarg.h>
 #include <stdio.h>
@@ -682,6 +684,22 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     return FMGI_OK;
 }
 
+/* frees the STREAM buffers (codes, slice-sorted copy, run tables); the next bake allocates them again */
+static void release_stream_buffers(fmgi_context *c) {
+    if (!c || c->device == FMGI_HOST_ONLY || hipSetDevice(c->device) != hipSuccess) return;
+    (void)hipStreamSynchronize(c->stream);
+    if (c->fold_stream) (void)hipStreamSynchronize(c->fold_stream);
+    for (int k = 0; k < 2; k++) {
+        (void)hipFree(c->sb[k].stream);
+        (void)hipFree(c->sb[k].sorted);
+        (void)hipFree(c->sb[k].toff);
+        c->sb[k].stream = c->sb[k].sorted = nullptr;
+        c->sb[k].toff = nullptr;
+        c->sb_cap_alloc[k] = 0;
+        c->sb_entries_alloc[k] = 0;
+    }
+}
+
 FMGI_API int fmgi_set_accumulation(fmgi_context *c, int mode) {
     if (!c || mode < FMGI_ACCUM_AUTO || mode > FMGI_ACCUM_STREAM) return set_err(FMGI_ERR_ARG, "bad accumulation mode");
     c->accum_req = mode;
@@ -753,6 +771,9 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->grid_cells = (int)gb.cells.size();
     c->grid_entries = (int)gb.idx.size();
     c->h_grid = gb;
+    /* ScanHybrid's image is the filter image followed by the plane image: its size must be this scene's
+       before the AUTO choice below asks which images fit LDS (also in host-only contexts) */
+    c->himg_bytes = c->fimg_bytes + c->gimg_bytes;
     {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
@@ -819,7 +840,6 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
         hipFree(c->d_himg);
         c->d_himg = nullptr;
         HIPCHK(upload(&c->d_himg, both));
-        c->himg_bytes = (int)both.size();
     }
     hipFree(c->d_gimg_cells);
     c->d_gimg_cells = nullptr;
@@ -1555,7 +1575,10 @@ static void dropin_release_shard(DropinShard &S) {
 static fmgi_context *g_plan_ctx = nullptr;
 static uint64_t g_plan_hash = 0;
 
+static void rccl_release();
+
 static void dropin_release_locked() {
+    rccl_release();
     fmgi_destroy(g_plan_ctx);
     g_plan_ctx = nullptr;
     g_plan_hash = 0;
@@ -1596,6 +1619,79 @@ static void enable_peer(int dev, int peer) {
         if (e == hipSuccess || e == hipErrorPeerAccessAlreadyEnabled) g_peer_on[dev][peer] = true;
         (void)hipGetLastError(); /* an "already enabled" must not linger as the thread's last error */
     }
+}
+
+/*
+ * RCCL for the drop-in's one-process multi-GPU reduce (ncclCommInitAll over the shard devices,
+ * one ncclReduce of the int64 lightmaps to shard 0 over xGMI). librccl is opened on the first call that
+ * needs it, so single-GPU callers of the library never load it; the communicators are cached with the
+ * shards (fmgi_dropin_release destroys them).
+ */
+struct RcclApi {
+    void *h = nullptr;
+    decltype(&ncclCommInitAll) comm_init_all = nullptr;
+    decltype(&ncclCommDestroy) comm_destroy = nullptr;
+    decltype(&ncclCommCount) comm_count = nullptr;
+    decltype(&ncclReduce) reduce = nullptr;
+    decltype(&ncclGroupStart) group_start = nullptr;
+    decltype(&ncclGroupEnd) group_end = nullptr;
+    decltype(&ncclGetErrorString) error_string = nullptr;
+};
+
+static const RcclApi *rccl_api() {
+    static RcclApi api;
+    static bool tried = false;
+    if (!tried) {
+        tried = true;
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) h = dlopen("librccl.so", RTLD_NOW | RTLD_LOCAL);
+        if (h) {
+            api.comm_init_all = (decltype(api.comm_init_all))dlsym(h, "ncclCommInitAll");
+            api.comm_destroy = (decltype(api.comm_destroy))dlsym(h, "ncclCommDestroy");
+            api.comm_count = (decltype(api.comm_count))dlsym(h, "ncclCommCount");
+            api.reduce = (decltype(api.reduce))dlsym(h, "ncclReduce");
+            api.group_start = (decltype(api.group_start))dlsym(h, "ncclGroupStart");
+            api.group_end = (decltype(api.group_end))dlsym(h, "ncclGroupEnd");
+            api.error_string = (decltype(api.error_string))dlsym(h, "ncclGetErrorString");
+            if (api.comm_init_all && api.comm_destroy && api.comm_count && api.reduce && api.group_start &&
+                api.group_end && api.error_string)
+                api.h = h;
+        }
+    }
+    return api.h ? &api : nullptr;
+}
+
+static std::vector<ncclComm_t> g_rccl_comms; /* one per shard, over the shard devices in shard order */
+static std::vector<int> g_rccl_devs;
+
+static void rccl_release() {
+    const RcclApi *R = rccl_api();
+    if (R)
+        for (ncclComm_t cm : g_rccl_comms) (void)R->comm_destroy(cm);
+    g_rccl_comms.clear();
+    g_rccl_devs.clear();
+}
+
+/* communicators over `devs` (distinct devices; rank k = shard k), created once per device list */
+static int rccl_comms(const std::vector<int> &devs) {
+    if (g_rccl_devs == devs && g_rccl_comms.size() == devs.size()) return FMGI_OK;
+    rccl_release();
+    const RcclApi *R = rccl_api();
+    if (!R) return set_err(FMGI_ERR_HIP, "librccl could not be loaded (FMGI_REDUCE=peer reduces by xGMI peer copies)");
+    std::vector<ncclComm_t> cm(devs.size());
+    const ncclResult_t r = R->comm_init_all(cm.data(), (int)devs.size(), devs.data());
+    if (r != ncclSuccess) return set_err(FMGI_ERR_HIP, "ncclCommInitAll over %zu devices: %s", devs.size(), R->error_string(r));
+    g_rccl_comms = cm;
+    g_rccl_devs = devs;
+    return FMGI_OK;
+}
+
+/* ranks of the cached communicator (ncclCommCount of rank 0's), 0 if none */
+FMGI_API int fmgi_dropin_rccl_ranks(void) {
+    const RcclApi *R = rccl_api();
+    int n = 0;
+    if (!R || g_rccl_comms.empty() || R->comm_count(g_rccl_comms[0], &n) != ncclSuccess) return 0;
+    return n;
 }
 
 /* the stream-accumulation overflow flag of a context's bakes since its reset (never set by sizing; a set
@@ -1688,8 +1784,19 @@ static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_ou
     int rc_all;
     {
         rc_all = bake_geometry_devices(geo, spa, wg, kernel, offs, items, texels_out, verbose);
+        /* FMGI_DROPIN_CACHE: 0 = free all device state after the call (the reference's behaviour,
+           global_illumination_cl.c:315-320); 1 (default) = keep the per-geometry state (contexts, scene
+           tables, lightmaps: a few MB per shard) but free the deposit-code stream buffers, which are
+           sized to the call's photon count (tens of GB at 1e9 photons); 2 = keep everything (repeated
+           bakes of large photon counts in one process) */
         const char *ce = getenv("FMGI_DROPIN_CACHE");
-        if (rc_all != FMGI_OK || (ce && atoi(ce) == 0)) dropin_release_locked();
+        const int cache = ce ? atoi(ce) : 1;
+        if (rc_all != FMGI_OK || cache <= 0) {
+            dropin_release_locked();
+        } else if (cache == 1) {
+            for (DropinShard &S : g_dropin)
+                if (S.ctx) release_stream_buffers(S.ctx);
+        }
     }
     guard.restore();
     return rc_all;
@@ -1785,9 +1892,35 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
         fflush(stdout);
     }
     if (geo->numTexels <= 0) return FMGI_OK;
+    /* the shards' lightmaps summed into shard 0: one RCCL reduce over the shard devices (default when every
+       shard has a device of its own), or a binary tree of xGMI peer copies + adds (FMGI_REDUCE=peer, and
+       shards sharing a device: RCCL allows one rank per GPU). FMGI_REDUCE=rccl forces RCCL, also for a
+       single shard (a one-rank communicator: the in-place reduce leaves the lightmap as it is). */
+    const char *r_env = getenv("FMGI_REDUCE");
+    bool distinct = true;
+    for (int k = 0; k < nshard; k++)
+        for (int j = 0; j < k; j++) distinct = distinct && sdev[(size_t)k] != sdev[(size_t)j];
+    const bool force_rccl = r_env && !strcmp(r_env, "rccl"), force_peer = r_env && !strcmp(r_env, "peer");
+    if (force_rccl && !distinct) return set_err(FMGI_ERR_ARG, "FMGI_REDUCE=rccl needs one shard per device");
+    const bool use_rccl = force_rccl || (nshard > 1 && distinct && !force_peer);
+    if (use_rccl) {
+        int rc = rccl_comms(std::vector<int>(sdev.begin(), sdev.end()));
+        if (rc != FMGI_OK) return rc;
+        const RcclApi *R = rccl_api();
+        ncclResult_t r = R->group_start();
+        for (int k = 0; k < nshard && r == ncclSuccess; k++) {
+            DropinShard &S = g_dropin[(size_t)k];
+            /* rank k's stream already holds its bake; the reduce follows it there (root: in place) */
+            r = R->reduce(S.lm, g_dropin[0].lm, (size_t)geo->numTexels * 4, ncclInt64, ncclSum, 0,
+                          g_rccl_comms[(size_t)k], S.ctx->stream);
+        }
+        const ncclResult_t r2 = R->group_end();
+        if (r == ncclSuccess) r = r2;
+        if (r != ncclSuccess) return set_err(FMGI_ERR_HIP, "ncclReduce of the shard lightmaps: %s", R->error_string(r));
+    }
     /* binary-tree reduction into shard 0 (fmgi_dropin_reduce_order), ordered by events across devices */
     std::vector<int32_t> rdst((size_t)nshard), rsrc((size_t)nshard);
-    const int nsteps = fmgi_dropin_reduce_order(nshard, rdst.data(), rsrc.data());
+    const int nsteps = use_rccl ? 0 : fmgi_dropin_reduce_order(nshard, rdst.data(), rsrc.data());
     {
         for (int i = 0; i < nsteps; i++) {
             DropinShard &D = g_dropin[(size_t)rdst[(size_t)i]], &Src = g_dropin[(size_t)rsrc[(size_t)i]];
@@ -1806,6 +1939,17 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
             if (e == hipSuccess) e = hipEventRecord(D.done, D.ctx->stream);
             if (e != hipSuccess) return set_err(FMGI_ERR_HIP, "shard reduction: %s", hipGetErrorString(e));
         }
+    }
+    /* every shard's bake and the reduction done: a stream overflow fails the call before the caller's
+       texels are touched */
+    for (int k = 0; k < nshard; k++) {
+        fmgi_context *ck = g_dropin[(size_t)k].ctx;
+        HIPCHK(hipSetDevice(ck->device));
+        HIPCHK(hipStreamSynchronize(ck->stream));
+    }
+    for (int k = 0; k < nshard; k++) {
+        const int rc = check_no_overflow(g_dropin[(size_t)k].ctx);
+        if (rc != FMGI_OK) return rc;
     }
     /* texels: the caller's values + the exact sum, rounded once (k_finalize), on shard 0's device */
     fmgi_context *c0 = S0.ctx;
@@ -1829,10 +1973,6 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
     if (rc != FMGI_OK) return rc;
     HIPCHK(hipMemcpyAsync(texels_out, g_dropin_tex, tb, hipMemcpyDeviceToHost, c0->stream));
     HIPCHK(hipStreamSynchronize(c0->stream));
-    for (int k = 0; k < nshard; k++) {
-        rc = check_no_overflow(g_dropin[(size_t)k].ctx);
-        if (rc != FMGI_OK) return rc;
-    }
     return FMGI_OK;
 }
 

@@ -259,9 +259,11 @@ struct ScanFastT {
         filter_axis<0, Coop>(lds, a.fJ[0], sub, coop, src, dir, L1, L2, code1);
         filter_axis<1, Coop>(lds + 64 * a.fJ[0], a.fJ[1], sub, coop, src, dir, L1, L2, code1);
         filter_axis<2, Coop>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], sub, coop, src, dir, L1, L2, code1);
-        /* rects that are not axis-aligned: exact order-independent tests (no early-out) */
-        cptr<int32_t> G = (cptr<int32_t>)a.general;
-        for (int g = 0; g < a.ngeneral; g++) {
+        /* rects that are not axis-aligned: exact order-independent tests (no early-out); coop lanes split
+           them like the filter records (each tested by one sub-lane, so coop_merge's L2 is the true
+           runner-up and a winning general rect does not look tied with itself) */
+        const int32_t *G = a.general;
+        for (int g = sub; g < a.ngeneral; g += coop) {
             const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
@@ -1003,6 +1005,9 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     const bool lead = !Scan::kCoop || ((int)__lane_id() & (a.coop - 1)) == 0;
 
     sst.clk.reset();
+#ifdef FMGI_CLOCK_STAMP /* diagnostic build: the in-kernel clock (MI355X_MICROARCH.md, DVFS item 6) */
+    const unsigned long long ck_t0 = __builtin_amdgcn_s_memtime(), ck_r0 = __builtin_amdgcn_s_memrealtime();
+#endif
     for (;;) {
         /* ---- stage 1: new photon (and new work item), then the iteration's one direction sample ---- */
         float edx = 0, edy = 0;
@@ -1141,6 +1146,15 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, ring, dep && lead, code);
         sst.clk.lap(ST_APPEND);
     }
+#ifdef FMGI_CLOCK_STAMP /* sum over waves of the shader-clock and 100-MHz deltas of the loop: stats[24], [25] */
+    {
+        const unsigned long long ck_t1 = __builtin_amdgcn_s_memtime(), ck_r1 = __builtin_amdgcn_s_memrealtime();
+        if ((threadIdx.x & 63) == 0) {
+            atomicAdd(a.stats + KSTAT_STAGE0 + 8, ck_t1 - ck_t0);
+            atomicAdd(a.stats + KSTAT_STAGE0 + 9, ck_r1 - ck_r0);
+        }
+    }
+#endif
     if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws, ring);
     if (TRACE && photon >= 0) {
         a.ev_counts[item - a.item_begin] = nev;

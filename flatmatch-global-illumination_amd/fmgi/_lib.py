@@ -19,6 +19,7 @@ EXPORTS = (
     "fmgi_dropin_release",
     "fmgi_dropin_shards",
     "fmgi_dropin_reduce_order",
+    "fmgi_dropin_rccl_ranks",
     "fmgi_version",
     "fmgi_last_error",
     "fmgi_device_count",
@@ -185,6 +186,7 @@ def load() -> C.CDLL:
         "fmgi_dropin_shards": (C.c_int, [C.c_uint64, C.c_int, C.c_int, vp, vp, vp]),
         "fmgi_dropin_reduce_order": (C.c_int, [C.c_int, vp, vp]),
         "fmgi_dropin_release": (None, []),
+        "fmgi_dropin_rccl_ranks": (C.c_int, []),
         "fmgi_device_sincosf_library": (C.c_int, [vp, vp, vp, vp, i64]),
         "fmgi_device_unit": (C.c_int, [vp, C.c_int, vp, vp, vp, i64]),
         "fmgi_grid_sizes": (C.c_int, [vp, vp]),

@@ -21,7 +21,10 @@
  *   FMGI_WG        virtual OpenCL work-group size of the launch schedule (default 256, the value
  *                  ROCm's OpenCL reports for CL_KERNEL_WORK_GROUP_SIZE; global_illumination_cl.c:300)
  *   FMGI_GPUS      number of GPUs one drop-in call shards over (default 1, like the reference; max 8)
- *   FMGI_KERNEL    "auto" (default), "grid", "fast" or "exact" -- all produce identical bits; see DESIGN.md
+ *   FMGI_REDUCE    how a multi-GPU call sums the shard lightmaps: "rccl" (default: one ncclReduce over
+ *                  the shard devices) or "peer" (binary tree of xGMI peer copies + adds)
+ *   FMGI_KERNEL    "auto" (default), "grid", "fast", "hybrid" or "exact" -- all produce identical bits
+ *   FMGI_DROPIN_CACHE  0, 1 (default) or 2: device state kept between calls (fmgi_dropin_release)
  *   FMGI_QUIET     1 = suppress the reference's progress line
  */
 #ifndef FLATMATCH_GI_H
@@ -61,9 +64,15 @@ void performGlobalIlluminationCl(fmgi_geometry *geo, int numSamplesPerArea);
    written to texels_out[numTexels] (initial values taken from geo->texels, which is not modified).
    Returns 0 on success, a negative fmgi error code otherwise (no exit()). */
 int getGlobalIlluminationCl(const fmgi_geometry *geo, int numSamplesPerArea, fmgi_vec3 *texels_out);
-/* The drop-in entry points keep their device state (contexts, scene tables, stream buffers) across
-   calls, keyed by the geometry; this frees it (FMGI_DROPIN_CACHE=0: freed after every call). */
+/* The drop-in entry points keep their per-geometry device state (contexts, scene tables, lightmaps; a
+   few MB per shard) across calls and free the deposit-code stream buffers at the end of every call
+   (FMGI_DROPIN_CACHE=1, the default); FMGI_DROPIN_CACHE=0 frees everything after every call, as the
+   reference does (global_illumination_cl.c:315-320); FMGI_DROPIN_CACHE=2 keeps the stream buffers too.
+   This frees all of it, and the RCCL communicators of a multi-GPU call. */
 void fmgi_dropin_release(void);
+/* Ranks of the RCCL communicator the last multi-GPU drop-in call reduced over (ncclCommCount; one rank
+   per shard device), 0 if that call reduced without RCCL. */
+int fmgi_dropin_rccl_ranks(void);
 /* The drop-in's multi-GPU layout (host only; for tests): shard k -> device dev[k], work items
    [begin[k], end[k]); and its binary-tree reduction into shard 0 (returns the step count, nshard - 1). */
 int fmgi_dropin_shards(uint64_t items, int ngpu, int nshard, int32_t *dev, uint64_t *begin, uint64_t *end);
@@ -140,14 +149,18 @@ enum {
    filter over every rect + exact verification; GRID = FAST's filter over per-plane grid cells only;
    HYBRID = GRID's cells for the floor/ceiling planes and FAST's filter for the walls. */
 enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2, FMGI_KERNEL_AUTO = 3, FMGI_KERNEL_HYBRID = 4 };
-/* AUTO = GRID when the scene has few planes for its rect count (closed boxes), else FAST. */
+/* AUTO = GRID when the scene has few planes for its rect count (closed boxes), HYBRID when only the
+   floor/ceiling records share few planes (apartment layouts), else FAST; a scan whose image does not
+   fit LDS falls back to one that does (EXACT needs none). */
 /* Deposit accumulation (both exact and order-free; results are identical):
    FX3   three int64 fixed-point atomics per deposit into the lightmap;
    STATE one u64 atomic per deposit into counts[colour state][texel] (8 KiB per texel of device memory),
          folded into the int64 lightmap at the end of every fmgi_bake_items;
    STREAM no atomics per deposit: 32-bit codes (texel << 10 | colour state) appended with coalesced
-         stores, then partitioned by 4096-texel tile and summed exactly in LDS (needs < 4,194,304 texels
-         and 2 x 12.8 GB of device memory: bakes run in chunks of 4e8 photons);
+         stores (sorted by 2048-texel fold tile in each wave's LDS ring when the lightmap has at most 63
+         tiles), then summed per tile exactly in LDS (needs < 4,194,304 texels; the codes of a chunk of
+         work items stay in HBM, 3.2 KB per work item at most, chunks sized to half of the free device
+         memory: one 1e9-photon chunk on an MI355X);
    AUTO  STREAM when the texel count allows it, else FX3;
    NONE  PROFILING ONLY: deposits are discarded (measures the tracing work alone; wrong lightmap). */
 enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2, FMGI_ACCUM_NONE = 3, FMGI_ACCUM_STREAM = 4 };
@@ -195,14 +208,16 @@ fmgi_context *fmgi_create(int device);
 void fmgi_destroy(fmgi_context *ctx);
 
 /* Upload the scene: wall rectangles (the rect list scanned by every photon) and the emitters
-   (windows first, then lights). Precomputes the per-rectangle constants on the host in IEEE fp32
-   exactly as photonmap.cl would compute them. */
+   (windows first, then lights). The per-rectangle values photonmap.cl derives with OpenCL builtins
+   (edge lengths, unit edges, sampler bases) are computed on the device by k_scene_setup with the
+   builtins' gfx950 instructions, so they carry the reference kernel's bits; the scan tables (filter
+   image, grid) are built on the host. */
 int fmgi_set_scene(fmgi_context *ctx, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
                    int num_windows, const fmgi_rect *lights, int num_lights, int num_texels);
 
 /* Select the accumulation mode (FMGI_ACCUM_*); takes effect for the current and later scenes. */
 int fmgi_set_accumulation(fmgi_context *ctx, int mode);
-/* The mode in effect (FMGI_ACCUM_FX3 or FMGI_ACCUM_STATE). */
+/* The mode in effect (FMGI_ACCUM_FX3, FMGI_ACCUM_STATE, FMGI_ACCUM_STREAM or FMGI_ACCUM_NONE). */
 int fmgi_get_accumulation(fmgi_context *ctx);
 
 /* Reference launch schedule for spa / wg. If rng_offsets is NULL, libc rand() is called once per
@@ -232,7 +247,7 @@ int fmgi_auto_kernel(const fmgi_context *ctx);
    by default. fmgi_get_timing synchronises, returns the sums since the previous call and resets them. */
 typedef struct {
     double bake_ms;         /* k_bake launches                                   */
-    double fold_ms;         /* STREAM fold (hist + scan + scatter + accumulate)  */
+    double fold_ms;         /* STREAM fold (k_tile_runs_pre, or k_slice_sort + k_tile_runs) */
     uint64_t bake_launches;
     uint64_t fold_launches;
 } fmgi_timing;
@@ -251,8 +266,9 @@ int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, 
    tooling. sizes[0..2] = plane pairs per axis (x, y, z), sizes[3] = cells, sizes[4] = overflow entries.
    fmgi_grid_copy fills (any pointer may be NULL):
      planes[2 * (sizes[0] + sizes[1] + sizes[2])]: per axis, pairs {plane of the +n class, plane of the
-       -n class}, each {float plane, u0, v0, iu, iv, mu, mv; int32 nu, nv, cell_off, pad[2]} (48 B;
-       mu = nu - 1, mv = nv - 1; NaN plane = padding);
+       -n class}, each {float plane, u0, v0, iu, iv, mu, mv; int32 nu, nv, cell_off; float ulo, uhi,
+       vlo, vhi (the records' box, rounded outward), pad[2]} (64 B; mu = nu - 1, mv = nv - 1; NaN
+       plane = padding);
      cells[sizes[3]] (48 B each): the cell's first two records {float cu, hwu, cv, hwv} (margin-grown
        extents; {0, -1, 0, -1} when absent), then {int32 count, rect index of record 0, of record 1,
        first overflow entry};

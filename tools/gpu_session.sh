@@ -14,6 +14,8 @@
 #   pmc              rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on a short bench ($PROF_ARGS)
 #   foldpmc          one rocprofv3 --pmc pass of LDS-pipe counters (the fold kernels' binding resource)
 #   sq               two rocprofv3 --pmc passes of SQ instruction / wait counters ($PROF_ARGS)
+#   grbm / tcp / sq3 one --pmc pass each: GRBM clock + SQ cycle split / TA-TD-TCP (vector memory path) / SQ memory issue
+#   clock            bench with the in-kernel clock build (make -C <pkg> variant VNAME=clock VFLAGS=-DFMGI_CLOCK_STAMP)
 # Each GPU step has its own time limit; a crash/timeout (rc > 1) stops the session.
 set -u
 cd "$(dirname "$0")/.."
@@ -47,6 +49,10 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU -d "$OUT/sq1" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step sq2 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_BRANCH -d "$OUT/sq2" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     foldpmc) step fold_lds 600 rocprofv3 --pmc SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_INSTS_LDS SQ_WAIT_INST_LDS SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_INSTS_VMEM_RD SQ_ACTIVE_INST_LDS -d "$OUT/fold_lds" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    grbm)  step grbm 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/grbm" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    tcp)   step tcp 600 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum GRBM_GUI_ACTIVE -d "$OUT/tcp" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    sq3)   step sq3 600 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA -d "$OUT/sq3" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    clock) step clock 600 env FMGI_LIB=clock python bench.py --steps 5 --warmup 3 --no-cpu-baseline ${PROF_ARGS:-} ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
   esac
