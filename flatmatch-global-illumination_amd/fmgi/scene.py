@@ -218,6 +218,27 @@ def shelves_scene(n_panels: int = 6000, tile_size: float = 4.0, seed: int = 7) -
     return Scene(f"shelves{n_panels}", walls, box.windows, box.lights, ntex)
 
 
+def tilted_scene(n_panels: int = 12, tile_size: float = 20.0, seed: int = 11) -> Scene:
+    """box200 plus n_panels rects that are not axis-aligned (vertical panels turned about z, and sloped
+    ones): every scan's `general` list (ScanFast / ScanGrid test them exactly), as a layout with
+    diagonal walls would give (parseLayout.c:48-128 registers a wall along any pixel direction)."""
+    box = box_scene(200, tile_size=tile_size)
+    rng = np.random.default_rng(seed)
+    walls = list(box.walls)
+    for i in range(n_panels):
+        x, y = f32(rng.uniform(1.5, 8.5)), f32(rng.uniform(1.5, 6.5))
+        a = rng.uniform(0.2, 1.4) + (np.pi if i % 2 else 0.0)
+        L = f32(rng.uniform(0.5, 1.5))
+        wx, wy = f32(L * np.cos(a)), f32(L * np.sin(a))
+        if i % 3 == 2:  # sloped: width along the floor, height rising
+            walls.append(create_rectangle(x, y, f32(0.3), wx, wy, 0, f32(-0.3 * wy), f32(0.3 * wx), f32(0.8), tile_size))
+        else:           # vertical, turned about z
+            walls.append(create_rectangle(x, y, f32(0.2), wx, wy, 0, 0, 0, f32(rng.uniform(0.8, 2.0)), tile_size))
+    walls = np.array(walls, RECT_DTYPE)
+    ntex = assign_texel_bases(walls)
+    return Scene(f"tilted{n_panels}", walls, box.windows, box.lights, ntex)
+
+
 def spa_for_photons(scene: Scene, photons: float) -> int:
     """numSamplesPerArea giving ~`photons` photons over the scene's emitters (main.c:58 semantics)."""
     area = 0.0

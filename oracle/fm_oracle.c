@@ -104,6 +104,26 @@ static v3 normalize3(v3 a) {
     }
     return vmul(s, ocml_rsqrt(d));
 }
+/*
+ * FMO_PORT (oracle/Makefile -> liboracle_port.so; bench.py's CPU baseline only): the same arithmetic, with
+ * the per-rect values photonmap.cl recomputes in every intersects() / getTileIdAt() / sampler call
+ * (length(width), width / length(width), ..., the sampler basis of the normal) computed once per bake with
+ * the same functions -- identical bits, a fraction of the work. The checker build leaves them per call,
+ * as the reference source has them.
+ */
+typedef struct { v3 wn, hn, bu, bv; float wl, hl; } fmo_pre;
+#ifdef FMO_PORT
+static const fmo_rect *g_pre_rects, *g_pre_srcs;
+static int g_pre_nrects, g_pre_nsrcs;
+static fmo_pre *g_pre_r, *g_pre_s;
+static inline const fmo_pre *pre_of(const fmo_rect *r) {
+    if (g_pre_r && r >= g_pre_rects && r < g_pre_rects + g_pre_nrects) return &g_pre_r[r - g_pre_rects];
+    if (g_pre_s && r >= g_pre_srcs && r < g_pre_srcs + g_pre_nsrcs) return &g_pre_s[r - g_pre_srcs];
+    return NULL;
+}
+#else
+static inline const fmo_pre *pre_of(const fmo_rect *r) { (void)r; return NULL; }
+#endif
 /* the reference HOST's length() (vector3_cl.c:93: sqrtf(x*x + y*y + z*z), gcc without FMA) */
 static float host_len3(v3 a) { return sqrtf(a.x * a.x + a.y * a.y + a.z * a.z); }
 
@@ -142,7 +162,7 @@ void fmo_sincos_n(const float *x, float *s, float *c, int64_t n) {
 }
 
 /* photonmap.cl:27-52 (sky, fold=1) and :54-74 (cosine, fold=0) */
-static v3 sample_hemisphere(uint32_t *rng, v3 ndir, int fold) {
+static v3 sample_hemisphere_b(uint32_t *rng, v3 ndir, const fmo_pre *q, int fold) {
     float r = sqrtf(fmo_rand(rng));
     float phi = 6.283184f * fmo_rand(rng); /* `2 * 3.141592f` folds exactly to 6.283184f */
     float sn, cs;
@@ -151,20 +171,47 @@ static v3 sample_hemisphere(uint32_t *rng, v3 ndir, int fold) {
     float v = r * sn;
     float n = sqrtf(1.0f - r * r);
     if (fold && u < 0) u = -u;
-    v3 udir = mk(0, 0, 1);
-    if (fabsf(dot3(udir, ndir)) >= 0.999999f) udir = mk(0, 1, 0);
-    v3 vdir = normalize3(cross3(udir, ndir));
-    udir = normalize3(cross3(vdir, ndir));
+    v3 udir, vdir;
+    if (q) {
+        udir = q->bu;
+        vdir = q->bv;
+    } else {
+        udir = mk(0, 0, 1);
+        if (fabsf(dot3(udir, ndir)) >= 0.999999f) udir = mk(0, 1, 0);
+        vdir = normalize3(cross3(udir, ndir));
+        udir = normalize3(cross3(vdir, ndir));
+    }
     return vadd(vadd(vmul(udir, u), vmul(vdir, v)), vmul(ndir, n));
+}
+
+/* photonmap.cl:43-48 (== :65-70): the sampler basis of a normal, and a rect's hoisted values */
+__attribute__((unused)) static void rect_pre(const fmo_rect *r, fmo_pre *q) {
+    v3 w = ld(r->width), h = ld(r->height), n = ld(r->n);
+    q->wl = len3(w);
+    q->hl = len3(h);
+    q->wn = vdiv(w, q->wl);
+    q->hn = vdiv(h, q->hl);
+    v3 udir = mk(0, 0, 1);
+    if (fabsf(dot3(udir, n)) >= 0.999999f) udir = mk(0, 1, 0);
+    q->bv = normalize3(cross3(udir, n));
+    q->bu = normalize3(cross3(q->bv, n));
 }
 
 /* photonmap.cl:95-120 */
 static int tile_at(const fmo_rect *r, v3 p) {
     v3 pDir = vsub(p, ld(r->pos));
-    v3 w = ld(r->width), h = ld(r->height);
-    float hLength = len3(w), vLength = len3(h);
-    float dx = dot3(vdiv(w, hLength), pDir);
-    float dy = dot3(vdiv(h, vLength), pDir);
+    const fmo_pre *q = pre_of(r);
+    float hLength, vLength, dx, dy;
+    if (q) {
+        hLength = q->wl, vLength = q->hl;
+        dx = dot3(q->wn, pDir);
+        dy = dot3(q->hn, pDir);
+    } else {
+        v3 w = ld(r->width), h = ld(r->height);
+        hLength = len3(w), vLength = len3(h);
+        dx = dot3(vdiv(w, hLength), pDir);
+        dy = dot3(vdiv(h, vLength), pDir);
+    }
     int W = r->lm[1], H = r->lm[2];
     int tx = (int)(dx * (float)W / hLength);
     int ty = (int)(dy * (float)H / vLength);
@@ -183,6 +230,14 @@ static float intersects(const fmo_rect *r, v3 src, v3 dir, float closest) {
     v3 ray = vmul(dir, fac);
     if (closest * closest < dot3(ray, ray)) return -1;
     v3 pDir = vsub(vadd(src, ray), pos);
+    const fmo_pre *q = pre_of(r);
+    if (q) {
+        float dx = dot3(q->wn, pDir);
+        if (dx < 0 || dx > q->wl) return -1;
+        float dy = dot3(q->hn, pDir);
+        if (dy < 0 || dy > q->hl) return -1;
+        return fac;
+    }
     v3 w = ld(r->width), h = ld(r->height);
     float wl = len3(w);
     float dx = dot3(vdiv(w, wl), pDir);
@@ -196,6 +251,7 @@ static float intersects(const fmo_rect *r, v3 src, v3 dir, float closest) {
 /* Deposit sink: either exact fixed point (lm_fx), fp32 (lm_f32) or an event log. */
 typedef struct sink {
     int64_t *lm_fx;
+    int64_t *counts; /* deposits per texel (fmo_bake_counts), or NULL */
     float *lm_f32;
     fmo_event *ev;
     int nev, cap;
@@ -218,7 +274,7 @@ static void trace_photon(uint32_t *rng, const fmo_rect *win, const fmo_rect *rec
     float dx = fmo_rand(rng);
     float dy = fmo_rand(rng);
     v3 wn = ld(win->n);
-    v3 dir = sample_hemisphere(rng, wn, isWindow);
+    v3 dir = sample_hemisphere_b(rng, wn, pre_of(win), isWindow);
     v3 pos = vadd(vadd(vadd(ld(win->pos), vmul(ld(win->width), dx)), vmul(ld(win->height), dy)),
                   vmul(dir, 1e-5f));
     k->st.photons++;
@@ -238,7 +294,7 @@ static void trace_photon(uint32_t *rng, const fmo_rect *win, const fmo_rect *rec
         int light_idx = h->lm[0] + tile;
         v3 hn = ld(h->n);
         if ((double)pos.z > 0.0005 || fmo_rand(rng) > 0.75f) {
-            dir = sample_hemisphere(rng, hn, 0);
+            dir = sample_hemisphere_b(rng, hn, pre_of(h), 0);
             if (pos.z < 1e-5f) {
                 color.x *= 1.0f;
                 color.y *= 0.85f;
@@ -250,6 +306,7 @@ static void trace_photon(uint32_t *rng, const fmo_rect *win, const fmo_rect *rec
             dir = vsub(dir, vmul(hn, two_d));
         }
         k->st.deposits++;
+        if (k->counts) k->counts[light_idx]++;
         if (k->lm_fx) {
             int64_t *t = k->lm_fx + 3 * (int64_t)light_idx;
             t[0] += to_fx(color.x, k);
@@ -346,9 +403,9 @@ static int64_t find_launch(const fmo_launch *L, int64_t nl, uint64_t item) {
     return lo;
 }
 
-void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const fmo_launch *launches,
-              int64_t nlaunches, uint64_t item_begin, uint64_t item_end, int64_t *lm_fx,
-              int64_t num_texels, int nthreads, fmo_stats *stats) {
+static void bake_impl(const fmo_rect *rects, int nrects, const fmo_rect *sources, const fmo_launch *launches,
+                      int64_t nlaunches, uint64_t item_begin, uint64_t item_end, int64_t *lm_fx,
+                      int64_t *counts, int64_t num_texels, int nthreads, fmo_stats *stats) {
     if (item_end <= item_begin || nlaunches <= 0) return;
 #ifdef _OPENMP
     int nt = nthreads > 0 ? nthreads : omp_get_max_threads();
@@ -357,14 +414,25 @@ void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const 
     (void)nthreads;
 #endif
     int64_t ntot = num_texels * 3;
+#ifdef FMO_PORT
+    int64_t nsrc = 0;
+    for (int64_t l = 0; l < nlaunches; l++) nsrc = launches[l].source + 1 > nsrc ? launches[l].source + 1 : nsrc;
+    g_pre_r = (fmo_pre *)malloc(sizeof(fmo_pre) * (size_t)(nrects > 0 ? nrects : 1));
+    g_pre_s = (fmo_pre *)malloc(sizeof(fmo_pre) * (size_t)(nsrc > 0 ? nsrc : 1));
+    for (int i = 0; i < nrects; i++) rect_pre(&rects[i], &g_pre_r[i]);
+    for (int64_t i = 0; i < nsrc; i++) rect_pre(&sources[i], &g_pre_s[i]);
+    g_pre_rects = rects, g_pre_nrects = nrects, g_pre_srcs = sources, g_pre_nsrcs = (int)nsrc;
+#endif
     fmo_stats tot;
     memset(&tot, 0, sizeof tot);
 #pragma omp parallel num_threads(nt)
     {
         int64_t *priv = (int64_t *)calloc((size_t)ntot, sizeof(int64_t));
+        int64_t *pcnt = counts ? (int64_t *)calloc((size_t)num_texels, sizeof(int64_t)) : NULL;
         sink k;
         memset(&k, 0, sizeof k);
         k.lm_fx = priv;
+        k.counts = pcnt;
 #pragma omp for schedule(dynamic, 64)
         for (int64_t w = (int64_t)item_begin; w < (int64_t)item_end; w++) {
             int64_t li = find_launch(launches, nlaunches, (uint64_t)w);
@@ -376,6 +444,8 @@ void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const 
 #pragma omp critical
         {
             for (int64_t i = 0; i < ntot; i++) lm_fx[i] += priv[i];
+            if (pcnt)
+                for (int64_t i = 0; i < num_texels; i++) counts[i] += pcnt[i];
             tot.photons += k.st.photons;
             tot.scans += k.st.scans;
             tot.deposits += k.st.deposits;
@@ -383,7 +453,13 @@ void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const 
             tot.inexact += k.st.inexact;
         }
         free(priv);
+        free(pcnt);
     }
+#ifdef FMO_PORT
+    free(g_pre_r);
+    free(g_pre_s);
+    g_pre_r = g_pre_s = NULL;
+#endif
     if (stats) {
         stats->photons += tot.photons;
         stats->scans += tot.scans;
@@ -391,6 +467,21 @@ void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const 
         stats->escapes += tot.escapes;
         stats->inexact += tot.inexact;
     }
+}
+
+void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const fmo_launch *launches,
+              int64_t nlaunches, uint64_t item_begin, uint64_t item_end, int64_t *lm_fx,
+              int64_t num_texels, int nthreads, fmo_stats *stats) {
+    bake_impl(rects, nrects, sources, launches, nlaunches, item_begin, item_end, lm_fx, NULL, num_texels, nthreads,
+              stats);
+}
+
+/* fmo_bake, also adding every texel's deposit count (photonmap.cl:257 executions) into counts[num_texels] */
+void fmo_bake_counts(const fmo_rect *rects, int nrects, const fmo_rect *sources, const fmo_launch *launches,
+                     int64_t nlaunches, uint64_t item_begin, uint64_t item_end, int64_t *lm_fx, int64_t *counts,
+                     int64_t num_texels, int nthreads, fmo_stats *stats) {
+    bake_impl(rects, nrects, sources, launches, nlaunches, item_begin, item_end, lm_fx, counts, num_texels, nthreads,
+              stats);
 }
 
 int fmo_trace_item(const fmo_rect *rects, int nrects, const fmo_rect *source, int is_window,

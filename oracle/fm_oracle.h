@@ -85,6 +85,10 @@ void fmo_bake(const fmo_rect *rects, int nrects, const fmo_rect *sources, const 
 
 /* Trace one work item (100 photons) starting from rng_state = gid + rng_offset, recording
    every bounce. Returns the number of events (<= cap are written). */
+/* fmo_bake, also adding each texel's deposit count into counts[num_texels] */
+void fmo_bake_counts(const fmo_rect *rects, int nrects, const fmo_rect *sources, const fmo_launch *launches,
+                     int64_t nlaunches, uint64_t item_begin, uint64_t item_end, int64_t *lm_fx, int64_t *counts,
+                     int64_t num_texels, int nthreads, fmo_stats *stats);
 int fmo_trace_item(const fmo_rect *rects, int nrects, const fmo_rect *source, int is_window,
                    uint32_t rng_state, fmo_event *ev, int cap, uint32_t *rng_final);
 

@@ -65,6 +65,9 @@ def load():
         lib.fmo_schedule.argtypes = [vp, C.c_int, C.c_int, C.c_int, C.c_int, vp, i64]
         lib.fmo_bake.restype = None
         lib.fmo_bake.argtypes = [vp, C.c_int, vp, vp, i64, u64, u64, vp, i64, C.c_int, C.POINTER(OracleStats)]
+        lib.fmo_bake_counts.restype = None
+        lib.fmo_bake_counts.argtypes = [vp, C.c_int, vp, vp, i64, u64, u64, vp, vp, i64, C.c_int,
+                                        C.POINTER(OracleStats)]
         lib.fmo_trace_item.restype = C.c_int
         lib.fmo_trace_item.argtypes = [vp, C.c_int, vp, C.c_int, C.c_uint32, vp, C.c_int, C.POINTER(C.c_uint32)]
         lib.fmo_trace_item_f32.restype = None
@@ -136,8 +139,10 @@ def schedule_with_offsets(scene, spa: int, offsets, wg: int = 256) -> np.ndarray
     return out
 
 
-def bake(scene, launches: np.ndarray, item_begin: int = 0, item_end: int | None = None, nthreads: int = 0):
-    """Exact fixed-point lightmap (int64 [numTexels, 3], units of 2^-25) of items [begin, end)."""
+def bake(scene, launches: np.ndarray, item_begin: int = 0, item_end: int | None = None, nthreads: int = 0,
+         counts: bool = False):
+    """Exact fixed-point lightmap (int64 [numTexels, 3], units of 2^-25) of items [begin, end);
+    counts=True also returns every texel's deposit count (int64 [numTexels])."""
     lib = load()
     if item_end is None:
         item_end = int(launches["item_begin"][-1] + launches["count"][-1]) if len(launches) else 0
@@ -146,8 +151,42 @@ def bake(scene, launches: np.ndarray, item_begin: int = 0, item_end: int | None 
     L = np.ascontiguousarray(launches, LAUNCH_DTYPE)
     lm = np.zeros((scene.num_texels, 3), np.int64)
     st = OracleStats()
+    if counts:
+        cnt = np.zeros(scene.num_texels, np.int64)
+        lib.fmo_bake_counts(_p(walls), len(walls), _p(src), _p(L), len(L), item_begin, item_end, _p(lm), _p(cnt),
+                            scene.num_texels, nthreads, C.byref(st))
+        return lm, st.as_dict(), cnt
     lib.fmo_bake(_p(walls), len(walls), _p(src), _p(L), len(L), item_begin, item_end, _p(lm), scene.num_texels,
                  nthreads, C.byref(st))
+    return lm, st.as_dict()
+
+
+_port = None
+
+
+def bake_port(scene, launches: np.ndarray, item_begin: int = 0, item_end: int | None = None, nthreads: int = 0):
+    """bake() through liboracle_port.so: the same restatement with the per-rect builtin values hoisted out
+    of the scan and FMA instructions (bit-identical, tests/test_oracle.py) -- bench.py's CPU baseline."""
+    global _port
+    load()
+    if _port is None:
+        vp, i64, u64 = C.c_void_p, C.c_int64, C.c_uint64
+        lib = C.CDLL(os.path.join(HERE, "liboracle_port.so"))
+        lib.fmo_bake.restype = None
+        lib.fmo_bake.argtypes = [vp, C.c_int, vp, vp, i64, u64, u64, vp, i64, C.c_int, C.POINTER(OracleStats)]
+        lib.fmo_set_hw_tables.restype = None
+        lib.fmo_set_hw_tables.argtypes = [vp, vp]
+        lib.fmo_set_hw_tables(_p(_hw_tables[0]), _p(_hw_tables[1]))
+        _port = lib
+    if item_end is None:
+        item_end = int(launches["item_begin"][-1] + launches["count"][-1]) if len(launches) else 0
+    walls = np.ascontiguousarray(scene.walls)
+    src = np.ascontiguousarray(scene.sources)
+    L = np.ascontiguousarray(launches, LAUNCH_DTYPE)
+    lm = np.zeros((scene.num_texels, 3), np.int64)
+    st = OracleStats()
+    _port.fmo_bake(_p(walls), len(walls), _p(src), _p(L), len(L), item_begin, item_end, _p(lm), scene.num_texels,
+                   nthreads, C.byref(st))
     return lm, st.as_dict()
 
 
@@ -215,10 +254,7 @@ def ref_kernel_available(variant: str = "strict") -> bool:
         os.path.join(HERE, "libref_runner.so"))
 
 
-def ref_run_items(scene, source: int, is_window: int, rng_states, variant: str = "strict") -> np.ndarray:
-    """Run the reference photonmap kernel (photonmap.cl:269) once per work item, each on a zeroed
-    lightColors buffer; returns float32 [n, numTexels, 4]. Variant "fast" is refused: built with the
-    reference's -cl-fast-relaxed-math it faults on the first escaping photon (see build_ref.sh)."""
+def _ref_open(variant: str):
     if variant not in ("strict", "relaxed"):
         raise ValueError(f"reference variant {variant!r} is not launchable")
     global _ref
@@ -228,9 +264,46 @@ def ref_run_items(scene, source: int, is_window: int, rng_states, variant: str =
         _ref.ref_last_error.restype = C.c_char_p
         _ref.ref_run_items.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
                                        C.c_void_p]
+        _ref.ref_run_sum.restype = C.c_longlong
+        _ref.ref_run_sum.argtypes = [C.c_void_p, C.c_void_p, C.c_int, C.c_int, C.c_int, C.c_void_p, C.c_int,
+                                     C.c_int, C.c_void_p]
     path = os.path.join(REF_DIR, f"photonmap_{variant}.hsaco")
     if _ref.ref_open(path.encode()) != 0:
         raise RuntimeError(_ref.ref_last_error().decode())
+    return _ref
+
+
+def ref_run_sum(scene, launches: np.ndarray, item_begin: int, item_end: int, variant: str = "strict",
+                streams: int = 16) -> np.ndarray:
+    """The race-free sum of the reference kernel's per-item lightmaps over flattened items [begin, end) of
+    a schedule (each item run alone on a zeroed buffer, as ref_run_items), exact in int64 fixed point
+    (units of 2^-25, [numTexels, 3]): what the reference computes for those items without its data race,
+    with its own per-item fp32 accumulation."""
+    ref = _ref_open(variant)
+    walls = np.ascontiguousarray(scene.walls)
+    srcs = np.ascontiguousarray(scene.sources)
+    out = np.zeros((scene.num_texels, 3), np.int64)
+    for L in launches:
+        lo, hi = max(int(L["item_begin"]), item_begin), min(int(L["item_begin"]) + int(L["count"]), item_end)
+        if lo >= hi:
+            continue
+        gids = np.arange(lo - int(L["item_begin"]), hi - int(L["item_begin"]), dtype=np.int64)
+        states = ((gids + int(L["rng_offset"])) & 0xFFFFFFFF).astype(np.uint32)
+        win = np.ascontiguousarray(srcs[int(L["source"]) : int(L["source"]) + 1])
+        bad = ref.ref_run_sum(_p(win), _p(walls), len(walls), scene.num_texels, int(L["is_window"]), _p(states),
+                              len(states), streams, _p(out))
+        if bad < 0:
+            raise RuntimeError(ref.ref_last_error().decode())
+        if bad:
+            raise RuntimeError(f"{bad} per-item texel values not multiples of 2^-25")
+    return out
+
+
+def ref_run_items(scene, source: int, is_window: int, rng_states, variant: str = "strict") -> np.ndarray:
+    """Run the reference photonmap kernel (photonmap.cl:269) once per work item, each on a zeroed
+    lightColors buffer; returns float32 [n, numTexels, 4]. Variant "fast" is refused: built with the
+    reference's -cl-fast-relaxed-math it faults on the first escaping photon (see build_ref.sh)."""
+    _ref = _ref_open(variant)
     walls = np.ascontiguousarray(scene.walls)
     win = np.ascontiguousarray(scene.sources[source : source + 1])
     rs = np.ascontiguousarray(rng_states, np.uint32)

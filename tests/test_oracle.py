@@ -112,3 +112,13 @@ def test_f32_item_matches_fixed_point_when_no_rounding(example_scene, libc):
     lm, _ = O.bake(example_scene, L, 7, 8)
     # the f32 sequential sum equals the exact sum up to fp32 rounding of the additions
     np.testing.assert_allclose(tex[:, :3], lm / 2**25, rtol=2e-7, atol=0)
+
+
+def test_port_build_is_bit_identical_to_the_oracle(box200, example_scene, libc):
+    """liboracle_port.so (bench.py's CPU baseline: per-rect builtin values hoisted out of the scan, FMA
+    instructions) computes exactly the oracle's lightmap and counters."""
+    for sc, spa, (b, e) in ((box200, 172_413_793, (0, 700)), (example_scene, 65_000, (9_000, 11_008))):
+        L = O.schedule(sc, spa)
+        a, sa = O.bake(sc, L, b, e)
+        p, sp = O.bake_port(sc, L, b, e)
+        assert np.array_equal(a, p) and sa == sp, sc.name

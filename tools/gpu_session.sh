@@ -4,6 +4,7 @@
 #   tests_k          pytest -m gpu $TESTS_ARGS (e.g. '-k radiosity')
 #   rad / radprof    tools/bench_rad.py $RAD_ARGS (plain / under rocprofv3 --kernel-trace --stats)
 #   ref              reference-kernel pin (tests/golden/make_ref_fixtures.py)
+#   tol              whole-launch reference sums, strict and relaxed (tests/golden/make_tolerance_fixtures.py)
 #   ocml             the device library's sin/cos digest (tests/golden/make_ocml_fixture.py)
 #   valu             VALU issue ceilings (tools/valu_peak)
 #   dropin           drop-in boundary timing, cached and uncached (tools/bench_dropin.py)
@@ -38,6 +39,7 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     rad)   step rad 900 python tools/bench_rad.py ${RAD_ARGS:-} ;;
     radprof) step radprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/radprof" -o run --output-format csv -- python tools/bench_rad.py --reps 1 --no-cpu-baseline ${RAD_ARGS:-} ;;
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;
+    tol)   step tol 1100 env GPU_MAX_HW_QUEUES=16 python -u tests/golden/make_tolerance_fixtures.py "$OUT" ;;
     ocml)  step ocml 300 python tests/golden/make_ocml_fixture.py "$OUT" ;;
     valu)  step valu 120 ./tools/valu_peak ;;
     dropin) step dropin 600 python tools/bench_dropin.py && step dropin_nocache 600 python tools/bench_dropin.py --no-cache ;;
