@@ -435,10 +435,8 @@ struct fmgi_context {
     int gimg_bytes = 0;
     int gJ[3] = {0, 0, 0};
     GridCell *d_gcells = nullptr;
-    char *d_gimg_cells = nullptr; /* plane image followed by the cells (FMGI_LDS_CELLS: both staged in LDS) */
     char *d_himg = nullptr;       /* ScanHybrid: the filter image followed by the grid's plane image */
     int himg_bytes = 0;
-    int gimg_cells_bytes = 0;
     float *d_grecs = nullptr;
     int32_t *d_gidx = nullptr;
     int grid_cells = 0, grid_entries = 0;
@@ -475,6 +473,13 @@ struct fmgi_context {
     int fetch_tab_cap = 0;
     std::vector<std::vector<uint32_t>> h_fetch_tab; /* the host side of each launch's table, kept for the call */
     std::vector<uint64_t> cost_items;               /* items per source of the measured call */
+    /* LDS staging blob of the scans: the scan image, then (optionally) copies of the RectDev and SrcDev
+       tables (plan_stage); rebuilt when the scene or the staging choice changes */
+    uint64_t scene_gen = 0;
+    char *d_blob = nullptr;
+    size_t blob_cap = 0;
+    uint64_t blob_key = ~0ull;
+    std::vector<RectLds> h_rects_lds; /* host staging of the LDS rect copy (kept until the copy is done) */
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -540,8 +545,8 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_general);
     hipFree(c->d_gimg);
     hipFree(c->d_gcells);
-    hipFree(c->d_gimg_cells);
     hipFree(c->d_himg);
+    hipFree(c->d_blob);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
     for (hipEvent_t ev : c->ev_pool) hipEventDestroy(ev);
@@ -722,6 +727,8 @@ static int bake_block() {
    launch fails; a scene whose image does not fit runs a kernel whose image does, or the exact scan (no
    image, identical results) */
 static const size_t kBakeLdsLimit = 65536;
+/* ... and with the limit raised (fmgi_launch_bake sets the kernel attribute): what staging may use */
+static const size_t kBakeLdsMax = 160 * 1024;
 
 static int image_bytes(const fmgi_context *c, int kernel) {
     return kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : (kernel == FMGI_KERNEL_HYBRID ? c->himg_bytes : c->fimg_bytes);
@@ -841,18 +848,6 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
         c->d_himg = nullptr;
         HIPCHK(upload(&c->d_himg, both));
     }
-    hipFree(c->d_gimg_cells);
-    c->d_gimg_cells = nullptr;
-    c->gimg_cells_bytes = 0;
-    if (const char *le = getenv("FMGI_LDS_CELLS")) {
-        if (atoi(le) > 0) {
-            std::vector<char> both((size_t)c->gimg_bytes + gb.cells.size() * sizeof(GridCell));
-            memcpy(both.data(), gb.img.data(), (size_t)c->gimg_bytes);
-            memcpy(both.data() + c->gimg_bytes, gb.cells.data(), gb.cells.size() * sizeof(GridCell));
-            HIPCHK(upload(&c->d_gimg_cells, both));
-            c->gimg_cells_bytes = (int)both.size();
-        }
-    }
     HIPCHK(upload(&c->d_grecs, gb.recs));
     HIPCHK(upload(&c->d_gidx, gb.idx));
     }
@@ -868,6 +863,7 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->num_texels = num_texels;
     c->h_launches.clear();
     c->total_items = 0;
+    c->scene_gen++;
     return FMGI_OK;
 }
 
@@ -970,13 +966,73 @@ FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
     return n;
 }
 
-static int lds_bytes(const fmgi_context *c, int kernel) { return image_bytes(c, kernel); }
+/*
+ * What a bake stages in LDS besides the scan image, and the workgroup size it runs with. Every photon
+ * emission reads its emitter's SrcDev and every scan's phase 2 reads the winner's RectDev; from global
+ * memory each is a dependent L2 round trip in the loop. A workgroup's LDS copy of the tables (128 B per
+ * emitter / wall) replaces them with LDS reads where the copy costs no occupancy: the emitters always
+ * (a few KB), the walls when some workgroup size keeps at least the resident waves the bake has without
+ * them (box200: 25.6 KB per workgroup; FMGI_RECTS_LDS=0/1 forces, FMGI_SRCS_LDS=0 turns the emitters off,
+ * FMGI_BLOCK fixes the workgroup size).
+ */
+struct StagePlan {
+    int block = 256;
+    int bytes = 0;                   /* staged blob = image (16-B aligned) | rects | srcs */
+    int rects_off = -1, srcs_off = -1;
+};
 
-static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, uint64_t items) {
+static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, int *roff, int *soff) {
+    int off = (image_bytes(c, kernel) + 15) & ~15;
+    if (roff) *roff = rects ? off : -1;
+    if (rects) off += c->nrects * (int)sizeof(RectLds);
+    if (soff) *soff = srcs ? off : -1;
+    if (srcs) off += c->nsrcs * (int)sizeof(SrcDev);
+    return off;
+}
+
+static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool trace) {
+    StagePlan p;
+    const char *be = getenv("FMGI_BLOCK");
+    const int forced_block = (be && atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) ? atoi(be) : 0;
+    p.block = forced_block ? forced_block : 256;
+    if (kernel == FMGI_KERNEL_EXACT) return p; /* no LDS image: nothing is staged */
+    const char *se = getenv("FMGI_SRCS_LDS"), *re = getenv("FMGI_RECTS_LDS");
+    const bool srcs = c->nsrcs > 0 && !(se && atoi(se) == 0);
+    const int rects_mode = re ? atoi(re) : -1; /* -1 auto */
+    const int kfn = kernel == FMGI_KERNEL_FAST && false ? kernel : kernel;
+    /* resident waves per CU of a (block, staged bytes) choice; 0 if it cannot launch */
+    auto waves = [&](int block, int bytes) -> int {
+        if (fmgi_bake_lds(kfn, accum, block, bytes, nullptr) > kBakeLdsMax) return 0;
+        return fmgi_bake_resident_blocks(kfn, accum, trace, block, bytes) * (block / 64);
+    };
+    const int blocks_all[] = {256, 512, 640, 768, 1024};
+    auto best = [&](bool rects, int &bb, int &bw) {
+        const int bytes = stage_bytes(c, kernel, rects, srcs, nullptr, nullptr);
+        bb = p.block;
+        bw = waves(p.block, bytes);
+        if (forced_block) return;
+        for (int B : blocks_all) {
+            const int w = waves(B, bytes);
+            if (w > bw) { bw = w; bb = B; }
+        }
+    };
+    int b0, w0, b1 = 0, w1 = 0;
+    best(false, b0, w0);
+    bool rects = false;
+    if (rects_mode != 0 && c->nrects > 0) {
+        best(true, b1, w1);
+        rects = rects_mode == 1 ? w1 > 0 : (w1 > 0 && w1 >= w0);
+    }
+    p.block = rects ? b1 : b0;
+    p.bytes = stage_bytes(c, kernel, rects, srcs, &p.rects_off, &p.srcs_off);
+    return p;
+}
+
+static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, int lds, uint64_t items) {
     /* persistent grid: exactly the blocks that are resident at once (occupancy from the VGPR/SGPR/LDS
        use of the kernel actually launched), so no block starts late and lengthens the tail; never more
        lanes than work items */
-    int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, lds_bytes(c, kernel));
+    int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, lds);
     if (per_cu <= 0) per_cu = 4;
     if (const char *pe = getenv("FMGI_BAKE_WG_PER_CU")) /* experiments: leave room for concurrent folds */
         if (atoi(pe) > 0) per_cu = std::min(per_cu, atoi(pe));
@@ -1036,18 +1092,20 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_HYBRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     const bool was_auto = kernel == FMGI_KERNEL_AUTO;
     if (was_auto) kernel = c->auto_kernel;
-    const int block = bake_block();
-    kernel = fitting_kernel(c, kernel, c->accum, block); /* an image too large for LDS: same results, other scan */
+    kernel = fitting_kernel(c, kernel, c->accum, bake_block()); /* an image too large for LDS: same results, other scan */
     if (b == e) return FMGI_OK;
     /* a launch with at most half as many items as resident lanes runs ScanFast with cooperative lanes
        (below): on such launches that beats the hybrid scan's single lane per item (config 1: 6.6 ms
        hybrid bake vs ~3.5 ms cooperative) */
     if (was_auto && kernel == FMGI_KERNEL_HYBRID && !trace && c->accum == FMGI_ACCUM_STREAM &&
-        fitting_kernel(c, FMGI_KERNEL_FAST, c->accum, block) == FMGI_KERNEL_FAST) {
+        fitting_kernel(c, FMGI_KERNEL_FAST, c->accum, bake_block()) == FMGI_KERNEL_FAST) {
+        const StagePlan fp = plan_stage(c, FMGI_KERNEL_FAST, c->accum, trace);
         const uint64_t lanes_max =
-            (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, c->accum, trace, block, UINT64_MAX) * block;
+            (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, c->accum, trace, fp.block, fp.bytes, UINT64_MAX) * fp.block;
         if ((e - b) * 2 <= lanes_max) kernel = FMGI_KERNEL_FAST;
     }
+    const StagePlan sp = plan_stage(c, kernel, c->accum, trace);
+    const int block = sp.block;
     if (c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     /* no walls: every photon escapes at its first scan (photonmap.cl:208), so nothing is deposited */
     if (c->nrects == 0) return FMGI_OK;
@@ -1072,11 +1130,6 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (kernel == FMGI_KERNEL_GRID) {
         a.fimg = c->d_gimg;
         a.fimg_bytes = c->gimg_bytes;
-        if (c->d_gimg_cells && fmgi_bake_lds(kernel, c->accum, block, c->gimg_cells_bytes, nullptr) <= kBakeLdsLimit) {
-            a.fimg = c->d_gimg_cells; /* GridPlane image (16-B multiple), then the cells */
-            a.fimg_bytes = c->gimg_cells_bytes;
-            a.cells_off = c->gimg_bytes;
-        }
         for (int k = 0; k < 3; k++) a.fJ[k] = c->gJ[k];
         a.gcells = c->d_gcells;
         a.grecs = c->d_grecs;
@@ -1100,6 +1153,50 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.fimg_bytes = c->fimg_bytes;
         for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
     }
+    a.rects_off = a.srcs_off = -1;
+    if (sp.rects_off >= 0 || sp.srcs_off >= 0) { /* the blob: image | RectDev table | SrcDev table */
+        const uint64_t key = (c->scene_gen << 8) | ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) |
+                             (sp.srcs_off >= 0 ? 1u : 0u);
+        if (c->blob_key != key) {
+            if (c->blob_cap < (size_t)sp.bytes) {
+                HIPCHK(hipStreamSynchronize(s)); /* no earlier bake may still stage the old blob */
+                hipFree(c->d_blob);
+                c->d_blob = nullptr;
+                c->blob_cap = 0;
+                HIPCHK(hipMalloc(&c->d_blob, (size_t)sp.bytes));
+                c->blob_cap = (size_t)sp.bytes;
+            }
+            if (a.fimg_bytes) HIPCHK(hipMemcpyAsync(c->d_blob, a.fimg, (size_t)a.fimg_bytes, hipMemcpyDeviceToDevice, s));
+            if (sp.rects_off >= 0) { /* RectDev -> RectLds (the device-computed fields, repacked) */
+                std::vector<RectDev> rd((size_t)c->nrects);
+                HIPCHK(hipStreamSynchronize(s));
+                HIPCHK(hipMemcpy(rd.data(), c->d_rects, rd.size() * sizeof(RectDev), hipMemcpyDeviceToHost));
+                c->h_rects_lds.assign((size_t)c->nrects, RectLds{});
+                for (size_t i = 0; i < rd.size(); i++) {
+                    const RectDev &r = rd[i];
+                    RectLds &q = c->h_rects_lds[i];
+                    q.px = r.px; q.py = r.py; q.pz = r.pz;
+                    q.nx = r.nx; q.ny = r.ny; q.nz = r.nz;
+                    q.wnx = r.wnx; q.wny = r.wny; q.wnz = r.wnz; q.wl = r.wl;
+                    q.hnx = r.hnx; q.hny = r.hny; q.hnz = r.hnz; q.hl = r.hl;
+                    q.base = r.base; q.W = r.W; q.H = r.H;
+                    q.bux = r.bux; q.buy = r.buy; q.buz = r.buz;
+                    q.bvx = r.bvx; q.bvy = r.bvy; q.bvz = r.bvz;
+                    q.iwl = r.iwl; q.ihl = r.ihl;
+                }
+                HIPCHK(hipMemcpyAsync(c->d_blob + sp.rects_off, c->h_rects_lds.data(),
+                                      c->h_rects_lds.size() * sizeof(RectLds), hipMemcpyHostToDevice, s));
+            }
+            if (sp.srcs_off >= 0)
+                HIPCHK(hipMemcpyAsync(c->d_blob + sp.srcs_off, c->d_srcs, (size_t)c->nsrcs * sizeof(SrcDev),
+                                      hipMemcpyDeviceToDevice, s));
+            c->blob_key = key;
+        }
+        a.fimg = c->d_blob;
+        a.fimg_bytes = sp.bytes;
+        a.rects_off = sp.rects_off;
+        a.srcs_off = sp.srcs_off;
+    }
     a.general = c->d_general;
     a.ngeneral = c->ngeneral;
     a.counts = c->accum == FMGI_ACCUM_STATE ? c->d_counts : nullptr;
@@ -1118,7 +1215,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             const int k = atoi(ce);
             a.coop = (k == 2 || k == 4 || k == 8) ? k : 1;
         } else {
-            const uint64_t lanes_max = (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block;
+            const uint64_t lanes_max =
+                (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block;
             while (a.coop < 8 && (e - b) * (uint64_t)a.coop * 2 <= lanes_max) a.coop *= 2;
         }
         if (a.coop > 1) kernel = FMGI_KERNEL_FAST_COOP;
@@ -1135,7 +1233,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int ns = c->nsrcs;
     /* only launches of at most 16 items per resident lane reorder (box200's 30 per lane: plain order) */
     const uint64_t order_lanes =
-        order_on ? (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block / (uint64_t)a.coop : 0;
+        order_on ? (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block /
+                       (uint64_t)a.coop
+                 : 0;
     if (order_on) {
         if (!c->ev_cost) HIPCHK(hipEventCreateWithFlags(&c->ev_cost, hipEventDisableTiming));
         if (c->cost_pending && hipEventQuery(c->ev_cost) == hipSuccess) { /* the previous measurement */
@@ -1222,7 +1322,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
         HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace,
-                                grid_blocks(c, kernel, c->accum, trace, block, (e - b) * (uint64_t)a.coop), block, s));
+                                grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop),
+                                block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
         if (a.counts)
@@ -1238,7 +1339,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
        and bake occupancy tried, because the persistent bake leaves the folds no room to run beside it,
        so the default is 1. */
     const uint64_t n = e - b;
-    const int lanes = grid_blocks(c, kernel, c->accum, trace, block, UINT64_MAX) * block;
+    const int lanes = grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block;
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
     /* presorted stream (bake-side counting sort by fold tile, no k_slice_sort pass): when the tiles fit
@@ -1264,7 +1365,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
         const int k = overlap ? (nchunk & 1) : 0; /* one buffer set unless the folds run beside the bakes */
-        const int grid = grid_blocks(c, kernel, c->accum, trace, block, (ce - cb) * (uint64_t)a.coop);
+        const int grid = grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, (ce - cb) * (uint64_t)a.coop);
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));

@@ -63,6 +63,22 @@ struct __attribute__((aligned(16))) RectDev {
 };
 static_assert(sizeof(RectDev) == 128, "RectDev must be 128 B");
 
+/* The fields of a RectDev the scans' phase 2 and the deposit read, as staged in LDS (BakeArgs::rects_off):
+   112 B = 28 dwords, so consecutive records start 28 banks apart (a 128-B stride puts every record's
+   field k on the same 4 banks: 64 lanes reading their winners' records then conflict up to 32 ways). */
+struct __attribute__((aligned(16))) RectLds {
+    float px, py, pz, nx;
+    float ny, nz, wnx, wny;
+    float wnz, wl, hnx, hny;
+    float hnz, hl;
+    int32_t base, W;
+    int32_t H;
+    float bux, buy, buz;
+    float bvx, bvy, bvz, iwl;
+    float ihl, pad0, pad1, pad2;
+};
+static_assert(sizeof(RectLds) == 112, "RectLds must be 112 B");
+
 /* One emitter (window or light), photonmap.cl:173-181. */
 struct __attribute__((aligned(16))) SrcDev {
     float px, py, pz, wx, wy, wz, hx, hy, hz, nx, ny, nz;

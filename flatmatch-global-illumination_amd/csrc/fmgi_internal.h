@@ -76,8 +76,10 @@ struct BakeArgs {
     const float *grecs;
     const int32_t *gridx;
     int grid_axes; /* fJ == {1, 1, 1}: slot a of the image is axis a (ScanGrid's grid_phase1_axes) */
-    int cells_off; /* > 0: the cells follow the plane image in LDS at this byte offset (else global) */
     int grid_xy_separate; /* layouts: walk the x and y planes one axis after the other (else merged) */
+    /* >= 0: byte offsets in the staged LDS blob (fimg) of a copy of the RectDev table (the phase-2 reads of
+       the scans' winners) and of the SrcDev table (every photon's emission); -1: read from global memory */
+    int rects_off, srcs_off;
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
     const uint32_t *fetch_tab;    /* fetch_nseg > 0: [f_begin, item_begin] pairs, f_begin ascending from 0:

@@ -18,6 +18,10 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <mutex>
+#include <set>
+#include <utility>
+
 #include "fmgi_internal.h"
 #include "flatmatch_gi.h"
 
@@ -29,6 +33,8 @@ namespace {
 
 template <class T>
 using cptr = const __attribute__((address_space(4))) T *; /* constant space: scalar loads */
+template <class T>
+using gptr = const __attribute__((address_space(1))) T *; /* global space: vector loads, never flat */
 
 struct LcgJumpC {
     uint32_t a[41], c[41];
@@ -93,9 +99,9 @@ struct HitRec {
     float bux, buy, buz, bvx, bvy, bvz;
 };
 
-/* photonmap.cl:123-158 (closest = INFINITY) on rect idx, filling h's rect fields and dx, dy */
-__device__ __forceinline__ float exact_hit(const BakeArgs &a, int idx, f3 src, f3 dir, HitRec &h) {
-    const RectDev &r = a.rects[idx];
+/* photonmap.cl:123-158 (closest = INFINITY) on rect r (index idx), filling h's rect fields and dx, dy */
+template <class R>
+__device__ __forceinline__ float exact_hit_rec(const R &r, int idx, f3 src, f3 dir, HitRec &h) {
     h.idx = idx;
     h.nx = r.nx; h.ny = r.ny; h.nz = r.nz;
     h.wl = r.wl; h.hl = r.hl;
@@ -105,6 +111,22 @@ __device__ __forceinline__ float exact_hit(const BakeArgs &a, int idx, f3 src, f
     h.bvx = r.bvx; h.bvy = r.bvy; h.bvz = r.bvz;
     return intersect_exact_uv(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz), mkf3(r.wnx, r.wny, r.wnz), r.wl,
                               mkf3(r.hnx, r.hny, r.hnz), r.hl, src, dir, h.dx, h.dy);
+}
+
+/* the same on rect idx, read from the workgroup's LDS copy of the table (RectLds records) when the host
+   staged it there (BakeArgs::rects_off >= 0), else from global memory; the two reads stay in their own address
+   spaces (a pointer that may be either compiles to flat loads, which wait on both counters) */
+__device__ __forceinline__ float exact_hit(const BakeArgs &a, const char *lds, int idx, f3 src, f3 dir, HitRec &h) {
+    if (a.rects_off >= 0)
+        return exact_hit_rec(((const __attribute__((address_space(3))) RectLds *)(
+                                 (const __attribute__((address_space(3))) char *)lds + a.rects_off))[idx],
+                             idx, src, dir, h);
+    return exact_hit_rec(((gptr<RectDev>)a.rects)[idx], idx, src, dir, h);
+}
+
+/* the global table (rare paths: fallbacks, ScanExact) */
+__device__ __forceinline__ float exact_hit(const BakeArgs &a, int idx, f3 src, f3 dir, HitRec &h) {
+    return exact_hit_rec(((gptr<RectDev>)a.rects)[idx], idx, src, dir, h);
 }
 
 /* the result of a literal scan (hit, best) as a HitRec (rare paths: ScanExact, fallbacks) */
@@ -262,7 +284,7 @@ struct ScanFastT {
         /* rects that are not axis-aligned: exact order-independent tests (no early-out); coop lanes split
            them like the filter records (each tested by one sub-lane, so coop_merge's L2 is the true
            runner-up and a winning general rect does not look tied with itself) */
-        const int32_t *G = a.general;
+        gptr<int32_t> G = (gptr<int32_t>)a.general;
         for (int g = sub; g < a.ngeneral; g += coop) {
             const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
@@ -282,13 +304,13 @@ struct ScanFastT {
         const int A = code1 >> 16, j = code1 & 0xFFFF;
         int idx;
         if (A == 3) {
-            idx = a.general[j];
+            idx = ((gptr<int32_t>)a.general)[j];
         } else {
             const float dA = A == 0 ? dir.x : (A == 1 ? dir.y : dir.z);
             const int off = A == 0 ? 0 : (A == 1 ? 64 * a.fJ[0] : 64 * (a.fJ[0] + a.fJ[1]));
             idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
         }
-        const float f = exact_hit(a, idx, src, dir, h);
+        const float f = exact_hit(a, lds, idx, src, dir, h);
         /* separation: the runner-up's phase-1 value must exceed the exact winner by > 2^-12 relative
            (covers the 2^-20 phase-1 error and the 2^-13 early-out slack); false for f = INF */
         if (!(f < 0) && L2 > f * 1.000244140625f) {
@@ -324,10 +346,11 @@ __device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, 
     return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)tv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)tu;
 }
 
-/* the grid cells: in LDS after the plane image when the host staged them there (BakeArgs::cells_off),
-   else in global memory */
-__device__ __forceinline__ const GridCell *grid_cells(const BakeArgs &a, const char *img) {
-    return a.cells_off ? (const GridCell *)(img + a.cells_off) : (const GridCell *)a.gcells;
+/* the grid cells, in global memory (L2-resident). Always a global pointer: a pointer that may point into
+   LDS or global memory compiles to flat loads, which count in both vmcnt and lgkmcnt and make every
+   LDS wait after them wait for the cell too (staging the cells in LDS was measured at +-0 %) */
+__device__ __forceinline__ const GridCell *grid_cells(const BakeArgs &a, const char *) {
+    return (const GridCell *)a.gcells;
 }
 
 /* one candidate test of ScanGrid's phase 1: record r against hit point (uh, vh) at fac' f */
@@ -657,7 +680,7 @@ struct ScanGrid {
             return;
         }
         const int idx = code1; /* rect index of the phase-1 winner */
-        const float f = exact_hit(a, idx, src, dir, h);
+        const float f = exact_hit(a, lds, idx, src, dir, h);
         const bool sep = !(f < 0) && L2 > f * 1.000244140625f; /* ScanFast's separation test */
         st.clk.lap(ST_SCAN2);
         if (sep) {
@@ -714,14 +737,14 @@ struct ScanHybrid {
         } else {
             const int A = code1 >> 16, j = code1 & 0xFFFF;
             if (A == 3) {
-                idx = a.general[j];
+                idx = ((gptr<int32_t>)a.general)[j];
             } else {
                 const float dA = A == 0 ? dir.x : dir.y;
                 const int off = A == 0 ? 0 : 64 * a.fJ[0];
                 idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
             }
         }
-        const float f = exact_hit(a, idx, src, dir, h);
+        const float f = exact_hit(a, lds, idx, src, dir, h);
         if (!(f < 0) && L2 > f * 1.000244140625f) { /* ScanFast's separation test */
             h.best = f;
             return;
@@ -959,6 +982,27 @@ __device__ __forceinline__ void locate_item(const BakeArgs &a, uint64_t w, int &
     gid = (uint32_t)(off % a.launch_cap);
 }
 
+/* the emitter fields photon emission reads (photonmap.cl:173-181 and the sampler basis) */
+template <class R>
+__device__ __forceinline__ SrcDev src_fields(const R &r) {
+    SrcDev d;
+    d.px = r.px; d.py = r.py; d.pz = r.pz;
+    d.wx = r.wx; d.wy = r.wy; d.wz = r.wz;
+    d.hx = r.hx; d.hy = r.hy; d.hz = r.hz;
+    d.nx = r.nx; d.ny = r.ny; d.nz = r.nz;
+    d.bux = r.bux; d.buy = r.buy; d.buz = r.buz;
+    d.bvx = r.bvx; d.bvy = r.bvy; d.bvz = r.bvz;
+    return d;
+}
+
+/* emitter srci: from the workgroup's LDS copy of the SrcDev table when staged (BakeArgs::srcs_off >= 0) */
+__device__ __forceinline__ SrcDev load_src(const BakeArgs &a, const char *lds, int srci) {
+    if (a.srcs_off >= 0)
+        return src_fields(((const __attribute__((address_space(3))) SrcDev *)(
+            (const __attribute__((address_space(3))) char *)lds + a.srcs_off))[srci]);
+    return src_fields(((gptr<SrcDev>)a.srcs)[srci]);
+}
+
 /* LCG^2: the two draws of a direction sample whose result is never used (last bounce) */
 __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
     constexpr uint32_t A2 = kJump.a[2], C2 = kJump.c[2];
@@ -1057,7 +1101,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 photon = -1;
                 nev = 0;
             }
-            const SrcDev &S = a.srcs[srci];
+            const SrcDev S = load_src(a, s_img, srci);
             col = win ? mkf3(18, 18, 18) : mkf3(16, 16, 18); /* photonmap.cl:167-169 */
             sid = win ? (512 + 1) : 1; /* colour state: source kind, then one bit per diffuse bounce */
             edx = rng_next(rng);
@@ -1073,7 +1117,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         sst.clk.lap(ST_START);
         if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
         if (start) {
-            const SrcDev &S = a.srcs[srci];
+            const SrcDev S = load_src(a, s_img, srci);
             pos = add3(add3(add3(mkf3(S.px, S.py, S.pz), mul3(mkf3(S.wx, S.wy, S.wz), edx)),
                             mul3(mkf3(S.hx, S.hy, S.hz), edy)),
                        mul3(dir, 1e-5f));
@@ -1379,11 +1423,28 @@ size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_
     return img + (accum == 4 ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
 
+/* a bake launch of more than 64 KiB of dynamic LDS (scan image + staged tables + rings, fmgi_api.cpp
+   plan_stage) needs the kernel's limit raised, once per (device, kernel instance) */
+static hipError_t bake_lds_attr(const void *fn, size_t lds) {
+    if (lds <= 65536) return hipSuccess;
+    static std::mutex mu;
+    static std::set<std::pair<int, const void *>> done;
+    int dev = 0;
+    hipError_t e = hipGetDevice(&dev);
+    if (e != hipSuccess) return e;
+    std::lock_guard<std::mutex> lk(mu);
+    if (done.count({dev, fn})) return hipSuccess;
+    e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (e == hipSuccess) done.insert({dev, fn});
+    return e;
+}
+
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes) {
     int n = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, bake_kernel(kernel, accum, trace), block,
-                                                     fmgi_bake_lds(kernel, accum, block, lds_bytes, nullptr)) !=
-        hipSuccess)
+    const void *fn = bake_kernel(kernel, accum, trace);
+    const size_t lds = fmgi_bake_lds(kernel, accum, block, lds_bytes, nullptr);
+    if (bake_lds_attr(fn, lds) != hipSuccess ||
+        hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, fn, block, lds) != hipSuccess)
         return 0;
     return n;
 }
@@ -1394,6 +1455,10 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
     int ring_off = 0;
     const size_t lds = fmgi_bake_lds(kernel, accum, block, a.fimg_bytes, &ring_off);
     if (ring_off != a.ring_off) return hipErrorInvalidValue; /* the caller sets a.ring_off from fmgi_bake_lds */
+    {
+        const hipError_t e = bake_lds_attr(bake_kernel(kernel, accum, trace), lds);
+        if (e != hipSuccess) return e;
+    }
     if (kernel == FMGI_KERNEL_FAST_COOP) {
         if (accum != 4 || trace) return hipErrorInvalidValue; /* cooperative lanes: stream accumulation only */
         launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);

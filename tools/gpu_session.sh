@@ -10,6 +10,8 @@
 #   dropin           drop-in boundary timing, cached and uncached (tools/bench_dropin.py)
 #   dropinprof       the same under rocprofv3 --kernel-trace --stats
 #   bench            python bench.py $BENCH_ARGS
+#   env_<tag>        bench.py (no CPU legs) under the environment assignments in $ENV_<TAG>
+#   ab               bench.py (no CPU legs) with each experiment build in $AB_LIBS (FMGI_LIB), then the default build
 #   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
 #   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
 #   pmc              rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on a short bench ($PROF_ARGS)
@@ -45,6 +47,9 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     dropin) step dropin 600 python tools/bench_dropin.py && step dropin_nocache 600 python tools/bench_dropin.py --no-cache ;;
     dropinprof) step dropinprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/dropinprof" -o run --output-format csv -- python tools/bench_dropin.py --reps 2 ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
+    ab)    for v in ${AB_LIBS:-base}; do step "ab_$v" 600 env FMGI_LIB=$v python bench.py --no-cpu-baseline ${AB_ARGS:-}; done &&
+           step ab_default 600 python bench.py --no-cpu-baseline ${AB_ARGS:-} ;;
+    env_*) v="ENV_$(echo "${s#env_}" | tr a-z A-Z)"; step "$s" 600 env ${!v} python bench.py --no-cpu-baseline ${AB_ARGS:-} ;;
     bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; step "$s" 600 python bench.py ${!v:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     pmclist) step pmclist 120 rocprofv3 -L ;;
