@@ -1005,7 +1005,9 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
         if (fmgi_bake_lds(kfn, accum, block, bytes, nullptr) > kBakeLdsMax) return 0;
         return fmgi_bake_resident_blocks(kfn, accum, trace, block, bytes) * (block / 64);
     };
-    const int blocks_all[] = {256, 512, 640, 768, 1024};
+    /* multiples of 4 waves only: a workgroup's waves are dealt to the CU's 4 SIMDs, and 10 waves (640
+       lanes) left SIMDs unevenly loaded (box200: 149.6 ms against 123.8 ms at 256, profiles/r03/s3) */
+    const int blocks_all[] = {256, 512, 1024};
     auto best = [&](bool rects, int &bb, int &bw) {
         const int bytes = stage_bytes(c, kernel, rects, srcs, nullptr, nullptr);
         bb = p.block;
@@ -1021,7 +1023,10 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     bool rects = false;
     if (rects_mode != 0 && c->nrects > 0) {
         best(true, b1, w1);
-        rects = rects_mode == 1 ? w1 > 0 : (w1 > 0 && w1 >= w0);
+        /* the walls in LDS take the winners' records off the vector-memory path, which is what binds the
+           bake (TA busy 98 %, profiles/r03/s3): worth a wave per SIMD (box200: 16 waves per CU with the
+           walls staged 77.6 ms, 20 waves without 123.8 ms), not two */
+        rects = rects_mode == 1 ? w1 > 0 : (w1 > 0 && w1 >= std::min(w0, 16));
     }
     p.block = rects ? b1 : b0;
     p.bytes = stage_bytes(c, kernel, rects, srcs, &p.rects_off, &p.srcs_off);
@@ -1280,14 +1285,23 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     auto fetch_table = [&](uint64_t cb, uint64_t ce) -> hipError_t { /* a.fetch_tab for items [cb, ce) */
         a.fetch_tab = nullptr;
         a.fetch_nseg = 0;
-        if (!order_on || c->src_cost_per_item.size() != (size_t)ns || (int)c->src_lo.size() != ns || ntab >= kMaxTabs ||
-            ce - cb > 16 * order_lanes || ce > 0xFFFFFFFFull)
+        if (!order_on || (int)c->src_lo.size() != ns || ntab >= kMaxTabs || ce - cb > 16 * order_lanes ||
+            ce > 0xFFFFFFFFull)
             return hipSuccess;
+        /* costs per item: measured on this context's previous bake, else the prior "lights, then windows,
+           each in reverse schedule order": a light's photons start inside the rooms and rarely escape, so
+           its items are the longest (example.png config 2: plain order 24.5 ms, this prior 21.6 ms, the
+           measured order 21.3 ms), and a one-shot call (main.c bakes once) gets most of the gain too */
+        std::vector<double> prior;
+        const std::vector<double> *cost = &c->src_cost_per_item;
+        if (c->src_cost_per_item.size() != (size_t)ns) {
+            prior.resize((size_t)ns);
+            for (int k = 0; k < ns; k++) prior[(size_t)k] = (k >= c->nwindows ? 1e9 : 0.0) + k;
+            cost = &prior;
+        }
         std::vector<int> ord((size_t)ns);
         for (int k = 0; k < ns; k++) ord[(size_t)k] = k;
-        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) {
-            return c->src_cost_per_item[(size_t)x] > c->src_cost_per_item[(size_t)y];
-        });
+        std::stable_sort(ord.begin(), ord.end(), [&](int x, int y) { return (*cost)[(size_t)x] > (*cost)[(size_t)y]; });
         std::vector<uint32_t> &h = c->h_fetch_tab[(size_t)ntab];
         h.clear();
         uint64_t f = 0;

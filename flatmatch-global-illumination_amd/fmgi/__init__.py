@@ -255,6 +255,11 @@ def dropin_release():
     load().fmgi_dropin_release()
 
 
+def dropin_rccl_ranks() -> int:
+    """Ranks of the RCCL communicator the last drop-in call reduced over (0: reduced without RCCL)."""
+    return int(load().fmgi_dropin_rccl_ranks())
+
+
 def dropin_shards(items: int, ngpu: int, nshard: int):
     """The drop-in's multi-GPU layout: (device, begin, end) per shard (fmgi_dropin_shards)."""
     dev = np.zeros(nshard, np.int32)

@@ -294,3 +294,51 @@ def test_multi_shard_drop_in_is_bit_identical(torch_cuda, box200, libc):
             del os.environ["FMGI_SHARDS"]
     assert np.array_equal(outs[0].view(np.uint32), outs[1].view(np.uint32))
     assert outs[0][:, :3].sum() > 0
+
+
+def test_rccl_reduce_path_and_cache_modes(torch_cuda, box200, libc):
+    """The drop-in's RCCL reduce (FMGI_REDUCE=rccl: ncclCommInitAll over the shard devices, one int64
+    ncclReduce into shard 0; on one GPU a one-rank communicator) gives the same texels as the default path;
+    shards that share a device refuse it (RCCL allows one rank per GPU) and reduce by peer copies instead.
+    FMGI_DROPIN_CACHE=1 (default) frees the stream buffers after the call, 2 keeps them."""
+    from fmgi._lib import FmgiError
+
+    spa = 2_000_000
+    fmgi.dropin_release()
+    libc.srand(1)
+    ref = fmgi.bake_geometry(box200, spa)
+    assert fmgi.dropin_rccl_ranks() == 0  # one shard, default: nothing to reduce
+    os.environ["FMGI_REDUCE"] = "rccl"
+    try:
+        libc.srand(1)
+        out = fmgi.bake_geometry(box200, spa)
+        assert fmgi.dropin_rccl_ranks() == 1
+        assert np.array_equal(out.view(np.uint32), ref.view(np.uint32))
+        os.environ["FMGI_SHARDS"] = "2"
+        libc.srand(1)
+        with pytest.raises(FmgiError, match="one shard per device"):
+            fmgi.bake_geometry(box200, spa)
+    finally:
+        os.environ.pop("FMGI_REDUCE", None)
+        os.environ.pop("FMGI_SHARDS", None)
+    fmgi.dropin_release()
+    assert fmgi.dropin_rccl_ranks() == 0
+    # device memory the call leaves behind: a few MB by default, the stream buffers (GBs) with cache 2
+    from fmgi import scene
+
+    example = scene.load_geometry(os.path.join(GOLDEN, "example_geometry.bin"), "example")
+    torch_cuda.cuda.synchronize()
+    free0 = torch_cuda.cuda.mem_get_info()[0]
+    libc.srand(1)
+    fmgi.bake_geometry(example, 6_500_000)  # BASELINE config 2: ~3 GB of deposit codes
+    free1 = torch_cuda.cuda.mem_get_info()[0]
+    assert free0 - free1 < (256 << 20), (free0 - free1) / 2**20
+    os.environ["FMGI_DROPIN_CACHE"] = "2"
+    try:
+        libc.srand(1)
+        fmgi.bake_geometry(example, 6_500_000)
+        free2 = torch_cuda.cuda.mem_get_info()[0]
+        assert free0 - free2 > (1 << 30), (free0 - free2) / 2**20
+    finally:
+        os.environ.pop("FMGI_DROPIN_CACHE", None)
+    fmgi.dropin_release()

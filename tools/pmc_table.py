@@ -16,7 +16,11 @@ import os
 
 
 def short(name):
-    return name.split("(")[0].strip()
+    """kernel name without its argument list and template arguments ("void (anonymous namespace)::k_bake<...>(...)"
+    -> "k_bake")"""
+    n = name.replace("(anonymous namespace)::", "")
+    n = n[5:] if n.startswith("void ") else n
+    return n.split("<")[0].split("(")[0].strip()
 
 
 def main():
