@@ -250,11 +250,97 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
     }
 }
 
+/* The fold of a chained stream (BakeArgs::presort == 2): tile t's codes are the blocks of its
+   FMGI_CHAIN_SHARDS chains, whole FMGI_CHAIN_BLOCK-code blocks except each chain's last. One workgroup per
+   (tile, group of blocks) reads its blocks with 16-B loads (a wave takes a block: 16 KB, 64 codes per
+   lane, all loads in flight before the first add) and sums them exactly in LDS as k_tile_runs does. */
+__global__ __launch_bounds__(1024) void k_chain_fold(const uint32_t *__restrict__ pool,
+                                                    const unsigned long long *__restrict__ fill,
+                                                    const uint32_t *__restrict__ tab, uint32_t kmax, int P, int G,
+                                                    const uint4 *__restrict__ colpack,
+                                                    unsigned long long *__restrict__ lm, int num_texels) {
+    constexpr uint32_t B = FMGI_CHAIN_BLOCK;
+    constexpr int X = FMGI_CHAIN_SHARDS;
+    extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
+    unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
+    uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
+    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
+    const int t = j % P, g = xcd + 8 * (j / P);
+    /* the tile's blocks: chain x holds min(ceil(fill / B), kmax) of them (positions past kmax blocks were
+       added to the lightmap directly) */
+    uint64_t nk[X], tot = 0;
+#pragma unroll
+    for (int x = 0; x < X; x++) {
+        const uint64_t f = fill[t * X + x];
+        nk[x] = min((f + B - 1) / B, (uint64_t)kmax);
+        tot += nk[x];
+    }
+    const uint64_t j_lo = tot * g / G, j_hi = tot * (g + 1) / G;
+    if (j_lo >= j_hi) return; /* uniform */
+    for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
+    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
+    __syncthreads();
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const int waves = blockDim.x >> 6;
+    for (uint64_t jj = j_lo + wave; jj < j_hi; jj += waves) {
+        int x = 0;
+        uint64_t k = jj;
+#pragma unroll
+        for (int y = 0; y < X - 1; y++)
+            if (x == y && k >= nk[y]) { k -= nk[y]; x = y + 1; }
+        const uint32_t v = tab[(uint64_t)(t * X + x) * kmax + k];
+        if (v == 0 || v == 0xFFFFFFFFu) continue; /* (never: every listed position got a block) */
+        const uint64_t f = fill[t * X + x];
+        const uint32_t len = (k + 1) * B <= f ? B : (uint32_t)(f - k * B);
+        const uint4 *blk = (const uint4 *)(pool + (uint64_t)(v - 1) * B);
+        uint4 q[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const uint32_t i4 = (uint32_t)(64 * u + lane); /* 16-B unit: codes 4 i4 .. 4 i4 + 3 */
+            q[u] = 4 * i4 < len ? blk[i4] : make_uint4(kSentinel, kSentinel, kSentinel, kSentinel);
+        }
+#pragma unroll
+        for (int u = 0; u < 16; u++) {
+            const uint32_t i0 = 4 * (uint32_t)(64 * u + lane);
+            const uint32_t cs[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                if (i0 + m >= len) continue;
+                const uint32_t c = cs[m];
+                const int tx = (int)((c >> 10) & (kTileTexels - 1));
+                const uint4 cc = col[c & 1023];
+                atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
+                if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
+                if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
+            }
+        }
+    }
+    __syncthreads();
+    for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
+        const int texel = t * kTileTexels + i;
+        if (texel >= num_texels) break;
+        const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
+        unsigned long long *qq = lm + 4 * (size_t)texel;
+        if (r) atomicAdd(qq + 0, r);
+        if (gg) atomicAdd(qq + 1, gg);
+        if (bb) atomicAdd(qq + 2, bb);
+    }
+}
+
 } // namespace
 
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s) {
     const int P = (num_texels + kTileTexels - 1) / kTileTexels;
     const size_t plds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16;
+    if (sb.presort == 2) {
+        hipError_t e = fmgi_set_lds_attr_once<3>((const void *)k_chain_fold, (int)plds);
+        if (e != hipSuccess) return e;
+        const int G = (sb.groups + 7) & ~7;
+        hipLaunchKernelGGL(k_chain_fold, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
+                           sb.stream, sb.chain_fill, sb.chain_tab, sb.kmax, P, G, (const uint4 *)sb.colpack, lm,
+                           num_texels);
+        return hipGetLastError();
+    }
     if (sb.presort) {
         hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre, (int)plds);
         if (e != hipSuccess) return e;

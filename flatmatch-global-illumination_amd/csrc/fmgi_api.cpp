@@ -566,6 +566,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
         hipFree(c->sb[k].sorted);
         hipFree(c->sb[k].cursor);
         hipFree(c->sb[k].toff);
+        hipFree(c->sb[k].chain_fill);
         if (c->ev_baked[k]) hipEventDestroy(c->ev_baked[k]);
         if (c->ev_folded[k]) hipEventDestroy(c->ev_folded[k]);
     }
@@ -637,29 +638,58 @@ static uint64_t stream_cap_for(uint64_t items, int grid, int block) {
     return items * FMGI_EVENTS_PER_ITEM + (waves + 1) * FMGI_STREAM_BLOCK;
 }
 
-static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block,
-                                       bool presort) {
-    return stream_cap_for(items, grid, block) > c->sb_cap_alloc[k] || (!presort && !c->sb[k].sorted);
+/* STREAM layouts (BakeArgs::presort): 0 = unsorted codes, folded through k_slice_sort's sorted copy;
+   1 = ring-sized segments presorted by tile; 2 = per-tile block chains (chain_out / k_chain_fold) */
+enum { kStreamSliced = 0, kStreamSegments = 1, kStreamChains = 2 };
+
+/* the chained stream's pool, in blocks: every code of the chunk, plus each chain's partly filled last block */
+static uint64_t chain_pool_blocks(uint64_t cap, int P) {
+    return (cap + FMGI_CHAIN_BLOCK - 1) / FMGI_CHAIN_BLOCK + (uint64_t)P * FMGI_CHAIN_SHARDS + 8;
+}
+/* block positions a chain may hold: 4x its even share (past them, codes go to the lightmap as atomics) */
+static uint32_t chain_kmax(uint64_t cap, int P) {
+    const uint64_t share = ((cap + FMGI_CHAIN_BLOCK - 1) / FMGI_CHAIN_BLOCK + (uint64_t)P * FMGI_CHAIN_SHARDS - 1) /
+                           ((uint64_t)P * FMGI_CHAIN_SHARDS);
+    return (uint32_t)std::min<uint64_t>(4 * share + 16, 0x7FFFFFFFull);
+}
+static uint64_t stream_alloc_codes(uint64_t cap, int P, int mode) {
+    return mode == kStreamChains ? chain_pool_blocks(cap, P) * FMGI_CHAIN_BLOCK : cap;
 }
 
-static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block, bool presort) {
+static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
+    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
+    return stream_alloc_codes(stream_cap_for(items, grid, block), P, mode) > c->sb_cap_alloc[k] ||
+           (mode == kStreamSliced && !c->sb[k].sorted);
+}
+
+static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
     StreamBufs &sb = c->sb[k];
     const uint64_t cap = stream_cap_for(items, grid, block);
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
-    /* run tables: per 8192-code slice (sorted by k_slice_sort), or per ring-sized segment (presorted) */
-    const uint64_t nslices = presort ? (cap + FMGI_RING_CODES - 1) / FMGI_RING_CODES
-                                     : (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
-    const uint64_t entries = (uint64_t)(P + 1) * nslices;
-    if (cap > c->sb_cap_alloc[k] || (!presort && !sb.sorted)) {
+    const uint64_t codes = stream_alloc_codes(cap, P, mode);
+    if (codes > c->sb_cap_alloc[k] || (mode == kStreamSliced && !sb.sorted)) {
         hipFree(sb.stream);
         hipFree(sb.sorted);
         sb.stream = sb.sorted = nullptr;
         c->sb_cap_alloc[k] = 0;
-        HIPCHK(hipMalloc(&sb.stream, cap * sizeof(uint32_t)));
-        if (!presort) HIPCHK(hipMalloc(&sb.sorted, cap * sizeof(uint32_t))); /* presorted: no second copy */
-        c->sb_cap_alloc[k] = cap;
+        HIPCHK(hipMalloc(&sb.stream, codes * sizeof(uint32_t)));
+        if (mode == kStreamSliced) HIPCHK(hipMalloc(&sb.sorted, codes * sizeof(uint32_t))); /* the sorted copy */
+        c->sb_cap_alloc[k] = codes;
     }
-    sb.presort = presort ? 1 : 0;
+    sb.presort = mode;
+    /* run tables: per 8192-code slice (sorted by k_slice_sort), or per ring-sized segment (presorted); the
+       chained stream's block tables instead */
+    uint64_t entries = 0;
+    if (mode == kStreamChains) {
+        sb.kmax = chain_kmax(cap, P);
+        sb.pool_blocks = chain_pool_blocks(cap, P);
+        entries = (uint64_t)P * FMGI_CHAIN_SHARDS * sb.kmax * 2; /* u32 entries, in u16 units */
+        if (!sb.chain_fill) HIPCHK(hipMalloc(&sb.chain_fill, (size_t)FMGI_MAX_TILES * FMGI_CHAIN_SHARDS * 8));
+    } else {
+        const uint64_t nslices = mode == kStreamSegments ? (cap + FMGI_RING_CODES - 1) / FMGI_RING_CODES
+                                                         : (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
+        entries = (uint64_t)(P + 1) * nslices;
+    }
     if (entries > c->sb_entries_alloc[k]) {
         hipFree(sb.toff);
         sb.toff = nullptr;
@@ -667,22 +697,28 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         HIPCHK(hipMalloc(&sb.toff, entries * sizeof(uint16_t)));
         c->sb_entries_alloc[k] = entries;
     }
+    sb.chain_tab = mode == kStreamChains ? (uint32_t *)sb.toff : nullptr;
     if (!sb.cursor) HIPCHK(hipMalloc(&sb.cursor, 64));
     sb.cap = cap;
     sb.colpack = c->d_colpack;
     /* the fold kernels run two 64-KiB workgroups per CU and tiles carry uneven code counts: ~8 (slice-
-       sorted) or ~16 (presorted) rounds of P x groups workgroups balance the tail (box200, 46 tiles,
-       presorted: 19.6 / 18.9 / 17.4 / 16.5 ms at 11 / 22 / 45 / 90 groups) */
+       sorted) or ~16 (presorted, chained) rounds of P x groups workgroups balance the tail (box200, 46
+       tiles, presorted: 19.6 / 18.9 / 17.4 / 16.5 ms at 11 / 22 / 45 / 90 groups) */
     {
         const int ncu = std::max(1, c->num_cus);
         const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
-        const int rounds = presort ? 16 : 8;
+        const int rounds = mode != kStreamSliced ? 16 : 8;
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
-           without a segment group, and each pays its LDS set-up and tile flush: at least 1024 segments
-           (64 per wave) per workgroup */
-        if (presort && !(ge && atoi(ge) > 0))
-            sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 1024));
+           without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
+           or 16 chain blocks (one per wave), per workgroup */
+        if (!(ge && atoi(ge) > 0)) {
+            if (mode == kStreamSegments)
+                sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 1024));
+            if (mode == kStreamChains)
+                sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
+                                                    std::max<uint64_t>(8, sb.pool_blocks / ((uint64_t)P * 16)));
+        }
         const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
     }
@@ -1074,10 +1110,12 @@ static hipError_t time_end(fmgi_context *c, hipStream_t s, hipEvent_t t0, hipEve
 
 /* work items per STREAM chunk: codes for 800 deposits per item, twice (stream + sorted), for each of the
    `sets` buffer sets in use, in at most half of the device memory that is free or already held by them */
-static uint64_t stream_chunk_items(fmgi_context *c, int sets, bool presort) {
+static uint64_t stream_chunk_items(fmgi_context *c, int sets, int mode) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
-    const double copies = presort ? 1.0 : 2.0; /* the stream, and the slice-sorted copy unless presorted */
+    /* the stream, and the slice-sorted copy of the unsorted layout (chains: the pool is the stream plus one
+       partly filled block per chain, and the block tables, within the 2 % allowance) */
+    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamChains ? 1.02 : 1.0);
     const double held = 4.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]) * (c->sb[0].sorted ? 2.0 : 1.0);
     const double avail = (double)fr + held;
     uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * copies * 4.0 * FMGI_EVENTS_PER_ITEM));
@@ -1356,12 +1394,15 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int lanes = grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block;
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
-    /* presorted stream (bake-side counting sort by fold tile, no k_slice_sort pass): when the tiles fit
-       one histogram entry per lane (FMGI_PRESORT=0 turns it off) */
+    /* the stream layout: per-tile chains (the bake's ring flush sorts by fold tile and appends each tile's
+       run to its chain; the fold reads whole blocks) when the tiles fit one histogram entry per lane, else
+       unsorted codes + k_slice_sort. FMGI_PRESORT=0/1/2 forces unsorted / presorted segments / chains. */
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
     const char *pre_env = getenv("FMGI_PRESORT");
-    const bool presort = P >= 1 && P <= FMGI_PRESORT_MAX_TILES && !(pre_env && atoi(pre_env) == 0);
-    uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, presort);
+    int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamChains : kStreamSliced;
+    if (pre_env && P >= 1 && P <= FMGI_PRESORT_MAX_TILES) smode = std::max(0, std::min(2, atoi(pre_env)));
+    if (pre_env && atoi(pre_env) == 0) smode = kStreamSliced;
+    uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, smode);
     if (const char *ce = getenv("FMGI_CHUNK_ITEMS")) /* tests: force several chunks */
         if (atoll(ce) > 0) chunk = std::min<uint64_t>(chunk, (uint64_t)atoll(ce));
     if (pipeline > 1) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>((n + pipeline - 1) / pipeline, 4 * (uint64_t)lanes));
@@ -1383,11 +1424,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));
-        if (ensure_stream_needs_growth(c, k, ce - cb, grid, block, presort)) { /* no fold may still read it */
+        if (ensure_stream_needs_growth(c, k, ce - cb, grid, block, smode)) { /* no fold may still read it */
             HIPCHK(hipStreamSynchronize(s));
             if (c->fold_stream) HIPCHK(hipStreamSynchronize(c->fold_stream));
         }
-        int rc = ensure_stream(c, k, ce - cb, grid, block, presort);
+        int rc = ensure_stream(c, k, ce - cb, grid, block, smode);
         if (rc != FMGI_OK) return rc;
         StreamBufs &sb = c->sb[k];
         a.item_begin = cb;
@@ -1395,9 +1436,19 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.stream = sb.stream;
         a.stream_cap = sb.cap;
         a.stream_cursor = sb.cursor;
-        a.presort = presort ? 1 : 0;
+        a.presort = smode;
         a.ntiles = P;
         a.toff = sb.toff;
+        a.colpack = (const uint4 *)c->d_colpack;
+        if (smode == kStreamChains) {
+            a.chain_fill = sb.chain_fill;
+            a.chain_tab = sb.chain_tab;
+            a.pool_cursor = sb.cursor;
+            a.pool_blocks = sb.pool_blocks;
+            a.kmax = sb.kmax;
+            HIPCHK(hipMemsetAsync(sb.chain_fill, 0, (size_t)P * FMGI_CHAIN_SHARDS * 8, s));
+            HIPCHK(hipMemsetAsync(sb.chain_tab, 0, (size_t)P * FMGI_CHAIN_SHARDS * sb.kmax * 4, s));
+        }
         HIPCHK(fetch_table(cb, ce));
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));

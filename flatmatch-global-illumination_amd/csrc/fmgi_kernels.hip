@@ -908,6 +908,103 @@ struct AccStream {
         ws.base += FMGI_RING_CODES;
     }
 
+    /* ---- chained stream (BakeArgs::presort == 2) ---- */
+    static constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+
+    /* the pool block of position k of chain c: allocated by the one reservation whose range holds the
+       block's first position (chain_reserve), published with an agent-scope store; a reader polls until
+       it appears (the allocating lane never waits before publishing, so the poll ends) */
+    static __device__ __forceinline__ uint32_t chain_block(const BakeArgs &a, uint32_t c, uint64_t k) {
+        if (k >= a.kmax) return kNoBlock;
+        uint32_t *slot = a.chain_tab + (uint64_t)c * a.kmax + k;
+        for (int it = 0; it < (1 << 22); it++) {
+            const uint32_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (v) return v == kNoBlock ? kNoBlock : v - 1;
+            __builtin_amdgcn_s_sleep(1);
+        }
+        atomicAdd(a.overflow, 1ull); /* never (bounded wait): the call fails instead of hanging */
+        return kNoBlock;
+    }
+    static __device__ __forceinline__ uint32_t chain_alloc(const BakeArgs &a, uint32_t c, uint64_t k) {
+        if (k >= a.kmax) return kNoBlock;
+        const unsigned long long b = atomicAdd(a.pool_cursor, 1ull);
+        const uint32_t v = b < a.pool_blocks ? (uint32_t)b + 1 : kNoBlock;
+        __hip_atomic_store(a.chain_tab + (uint64_t)c * a.kmax + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        return v == kNoBlock ? kNoBlock : (uint32_t)b;
+    }
+    /* n codes of chain c reserved at positions [p, p + n) (n <= FMGI_RING_CODES < FMGI_CHAIN_BLOCK, so at
+       most two blocks): allocates the block whose first position it holds, returns both blocks */
+    static __device__ __forceinline__ void chain_reserve(const BakeArgs &a, uint32_t c, uint64_t p, uint32_t n,
+                                                         uint32_t &b0, uint32_t &b1) {
+        constexpr uint64_t B = FMGI_CHAIN_BLOCK;
+        const uint64_t k0 = p / B, k1 = (p + n - 1) / B;
+        uint32_t mine = kNoBlock;
+        uint64_t km = ~0ull;
+        if (p % B == 0) km = k0;
+        else if (k1 > k0) km = k1;
+        if (km != ~0ull) mine = chain_alloc(a, c, km);
+        b0 = km == k0 ? mine : chain_block(a, c, k0);
+        b1 = k1 == k0 ? b0 : (km == k1 ? mine : chain_block(a, c, k1));
+    }
+    /* the rare fallback (a chain past kmax blocks, or the pool exhausted): the code's colour, added to
+       the int64 lightmap with device atomics (exact, order-free, as AccFx3) */
+    static __device__ __forceinline__ void chain_atomic(const BakeArgs &a, uint32_t code) {
+        const uint4 cc = a.colpack[code & 1023];
+        unsigned long long *q = a.lm + 4 * (size_t)(code >> 10);
+        const unsigned long long r = cc.x;
+        atomicAdd(q + 0, r);
+        atomicAdd(q + 1, r + (unsigned long long)(long long)(int32_t)cc.y);
+        atomicAdd(q + 2, r + (unsigned long long)(long long)(int32_t)cc.z);
+    }
+
+    /* chained stream: append ring[0, n) to the tiles' chains. An LDS histogram counts the codes per tile;
+       one lane per tile reserves its run in its chain with one atomic and resolves the run's blocks into
+       the wave's info table; every code then takes a rank in its run (a returning LDS add on the reset
+       histogram) and is stored at its position. Codes stay in the ring (no registers held across the
+       reservation). Called where every live lane of the wave is active. */
+    static __device__ __forceinline__ void chain_out(const BakeArgs &a, uint32_t *ring, uint32_t n) {
+        constexpr uint32_t B = FMGI_CHAIN_BLOCK;
+        uint32_t *hist = ring + FMGI_RING_CODES + 64;
+        uint4 *info = (uint4 *)(hist + 64); /* per tile {block 0, offset in it, codes that fit in it, block 1} */
+        const uint64_t live = __ballot(true);
+        const uint32_t nl = (uint32_t)__popcll(live);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
+        const int P = a.ntiles;
+        const uint32_t shift = 10 + FMGI_TILE_BITS, shard = blockIdx.x & (FMGI_CHAIN_SHARDS - 1);
+        for (uint32_t t = r; t < 64; t += nl) hist[t] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (int t = (int)r; t < P; t += (int)nl) {
+            const uint32_t cnt = hist[t];
+            uint4 inf = make_uint4(kNoBlock, 0u, 0u, kNoBlock);
+            if (cnt) {
+                const uint32_t c = (uint32_t)t * FMGI_CHAIN_SHARDS + shard;
+                const uint64_t p = atomicAdd(a.chain_fill + c, (unsigned long long)cnt);
+                uint32_t k0b, k1b;
+                chain_reserve(a, c, p, cnt, k0b, k1b);
+                inf = make_uint4(k0b, (uint32_t)(p % B), B - (uint32_t)(p % B), k1b);
+            }
+            info[t] = inf;
+            hist[t] = 0; /* the run's rank cursor from here on */
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        for (uint32_t k = r; k < n; k += nl) {
+            const uint32_t code = ring[k], t = code >> shift;
+            const uint32_t rk = atomicAdd(&hist[t], 1u);
+            const uint4 inf = info[t];
+            const bool first = rk < inf.z;
+            const uint32_t blk = first ? inf.x : inf.w;
+            if (blk == kNoBlock) chain_atomic(a, code);
+            else a.stream[(uint64_t)blk * B + (first ? inf.y + rk : rk - inf.z)] = code;
+        }
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+
     static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, uint32_t *ring, bool dep,
                                                   uint32_t code) {
         const uint64_t m = __ballot(dep);
@@ -919,7 +1016,8 @@ struct AccStream {
         ws.tot += n;
         if (fill + n < FMGI_RING_CODES) return;
         /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
-        if (a.presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
+        if (a.presort == 2) chain_out(a, ring, FMGI_RING_CODES);
+        else if (a.presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
         else copy_out(a, ws, ring, FMGI_RING_CODES);
         const uint32_t rest = fill + n - FMGI_RING_CODES; /* < n <= live lanes: one code per live lane */
         const uint64_t live = __ballot(true);
@@ -943,6 +1041,10 @@ struct AccStream {
         ws.end = __shfl(ws.end, src, 64);
         const uint32_t fill = ws.tot % FMGI_RING_CODES, padded = (fill + 3) & ~3u;
         const uint32_t lane = __lane_id();
+        if (a.presort == 2) { /* the last (partial) ring into the chains */
+            if (fill) chain_out(a, ring, fill);
+            return;
+        }
         if (a.presort) { /* the last (partial) ring, then empty run tables for the block's unused segments */
             if (fill) sorted_out(a, ws, ring, fill);
             const int P = a.ntiles;
