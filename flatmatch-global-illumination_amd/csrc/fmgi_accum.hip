@@ -250,58 +250,96 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
     }
 }
 
-/* The fold of a chained stream (BakeArgs::presort == 2): tile t's codes are the blocks of its
-   FMGI_CHAIN_SHARDS chains, whole FMGI_CHAIN_BLOCK-code blocks except each chain's last. One workgroup per
-   (tile, group of blocks) reads its blocks with 16-B loads (a wave takes a block: 16 KB, 64 codes per
-   lane, all loads in flight before the first add) and sums them exactly in LDS as k_tile_runs does. */
-__global__ __launch_bounds__(1024) void k_chain_fold(const uint32_t *__restrict__ pool,
-                                                    const unsigned long long *__restrict__ fill,
-                                                    const uint32_t *__restrict__ tab, uint32_t kmax, int P, int G,
-                                                    const uint4 *__restrict__ colpack,
-                                                    unsigned long long *__restrict__ lm, int num_texels) {
-    constexpr uint32_t B = FMGI_CHAIN_BLOCK;
-    constexpr int X = FMGI_CHAIN_SHARDS;
+/* The fold of a bucketed stream (BakeArgs::presort == 2). k_bucket_count / k_bucket_list group the pool's
+   blocks by tile (block_tile[] -> block_list[], each tile's blocks contiguous; one global atomic per tile
+   and workgroup), and k_bucket_fold gives each (tile, group of blocks) one workgroup: a wave takes a
+   whole 4-KB block (16 codes per lane, four 16-B loads, all in flight before the first add) and sums it
+   exactly in LDS as k_tile_runs does. */
+constexpr int kListThreads = 1024;
+constexpr int kListPerThread = 8;
+
+__global__ __launch_bounds__(kListThreads) void k_bucket_count(const uint32_t *__restrict__ block_tile,
+                                                               const unsigned long long *__restrict__ cursor,
+                                                               uint64_t pool_blocks, int P,
+                                                               uint32_t *__restrict__ counts) {
+    __shared__ uint32_t h[64];
+    const uint64_t nb = min(*cursor, pool_blocks);
+    const uint64_t b0 = (uint64_t)blockIdx.x * kListThreads * kListPerThread;
+    if (b0 >= nb) return; /* uniform */
+    if (threadIdx.x < 64) h[threadIdx.x] = 0;
+    __syncthreads();
+    for (int k = 0; k < kListPerThread; k++) {
+        const uint64_t b = b0 + (uint64_t)k * kListThreads + threadIdx.x;
+        if (b < nb) atomicAdd(&h[block_tile[b]], 1u);
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < P && h[threadIdx.x]) atomicAdd(&counts[threadIdx.x], h[threadIdx.x]);
+}
+
+__global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__restrict__ block_tile,
+                                                              const unsigned long long *__restrict__ cursor,
+                                                              uint64_t pool_blocks, int P,
+                                                              const uint32_t *__restrict__ counts,
+                                                              uint32_t *__restrict__ cursors,
+                                                              uint32_t *__restrict__ list) {
+    __shared__ uint32_t h[64], base[64];
+    const uint64_t nb = min(*cursor, pool_blocks);
+    const uint64_t b0 = (uint64_t)blockIdx.x * kListThreads * kListPerThread;
+    if (b0 >= nb) return; /* uniform */
+    if (threadIdx.x < 64) h[threadIdx.x] = 0;
+    __syncthreads();
+    uint32_t t[kListPerThread], rk[kListPerThread];
+    for (int k = 0; k < kListPerThread; k++) {
+        const uint64_t b = b0 + (uint64_t)k * kListThreads + threadIdx.x;
+        t[k] = b < nb ? block_tile[b] : 0xFFFFFFFFu;
+        rk[k] = t[k] != 0xFFFFFFFFu ? atomicAdd(&h[t[k]], 1u) : 0u;
+    }
+    __syncthreads();
+    if ((int)threadIdx.x < P) { /* this workgroup's range in tile t's part of the list */
+        uint32_t off = 0;
+        for (int u = 0; u < (int)threadIdx.x; u++) off += counts[u];
+        base[threadIdx.x] = h[threadIdx.x] ? off + atomicAdd(&cursors[threadIdx.x], h[threadIdx.x]) : 0u;
+    }
+    __syncthreads();
+    for (int k = 0; k < kListPerThread; k++)
+        if (t[k] != 0xFFFFFFFFu) list[base[t[k]] + rk[k]] = (uint32_t)(b0 + (uint64_t)k * kListThreads + threadIdx.x);
+}
+
+__global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict__ pool,
+                                                     const uint32_t *__restrict__ list,
+                                                     const uint32_t *__restrict__ block_len,
+                                                     const uint32_t *__restrict__ counts, int P, int G,
+                                                     const uint4 *__restrict__ colpack,
+                                                     unsigned long long *__restrict__ lm, int num_texels) {
+    constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
     unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
     const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
     const int t = j % P, g = xcd + 8 * (j / P);
-    /* the tile's blocks: chain x holds min(ceil(fill / B), kmax) of them (positions past kmax blocks were
-       added to the lightmap directly) */
-    uint64_t nk[X], tot = 0;
-#pragma unroll
-    for (int x = 0; x < X; x++) {
-        const uint64_t f = fill[t * X + x];
-        nk[x] = min((f + B - 1) / B, (uint64_t)kmax);
-        tot += nk[x];
-    }
-    const uint64_t j_lo = tot * g / G, j_hi = tot * (g + 1) / G;
+    uint32_t off = 0;
+    for (int u = 0; u < t; u++) off += counts[u];
+    const uint32_t nt = counts[t];
+    const uint32_t j_lo = (uint32_t)((uint64_t)nt * g / G), j_hi = (uint32_t)((uint64_t)nt * (g + 1) / G);
     if (j_lo >= j_hi) return; /* uniform */
     for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
     for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int waves = blockDim.x >> 6;
-    for (uint64_t jj = j_lo + wave; jj < j_hi; jj += waves) {
-        int x = 0;
-        uint64_t k = jj;
+    for (uint32_t jj = j_lo + wave; jj < j_hi; jj += waves) {
+        const uint32_t b = list[off + jj];
+        const uint32_t len = min(block_len[b], BP);
+        const uint4 *blk = (const uint4 *)(pool + (uint64_t)b * BP);
+        uint4 q[4];
 #pragma unroll
-        for (int y = 0; y < X - 1; y++)
-            if (x == y && k >= nk[y]) { k -= nk[y]; x = y + 1; }
-        const uint32_t v = tab[(uint64_t)(t * X + x) * kmax + k];
-        if (v == 0 || v == 0xFFFFFFFFu) continue; /* (never: every listed position got a block) */
-        const uint64_t f = fill[t * X + x];
-        const uint32_t len = (k + 1) * B <= f ? B : (uint32_t)(f - k * B);
-        const uint4 *blk = (const uint4 *)(pool + (uint64_t)(v - 1) * B);
-        uint4 q[16];
-#pragma unroll
-        for (int u = 0; u < 16; u++) {
-            const uint32_t i4 = (uint32_t)(64 * u + lane); /* 16-B unit: codes 4 i4 .. 4 i4 + 3 */
+        for (int u = 0; u < 4; u++) { /* 16-B unit i4 = 64 u + lane: codes 4 i4 .. 4 i4 + 3 */
+            const uint32_t i4 = 64 * u + lane;
             q[u] = 4 * i4 < len ? blk[i4] : make_uint4(kSentinel, kSentinel, kSentinel, kSentinel);
         }
 #pragma unroll
-        for (int u = 0; u < 16; u++) {
-            const uint32_t i0 = 4 * (uint32_t)(64 * u + lane);
+        for (int u = 0; u < 4; u++) {
+            const uint32_t i0 = 4 * (64 * u + lane);
             const uint32_t cs[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
             for (int m = 0; m < 4; m++) {
@@ -333,11 +371,20 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
     const int P = (num_texels + kTileTexels - 1) / kTileTexels;
     const size_t plds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16;
     if (sb.presort == 2) {
-        hipError_t e = fmgi_set_lds_attr_once<3>((const void *)k_chain_fold, (int)plds);
+        /* the blocks listed by tile (counts, then each workgroup's range in its tiles' parts), then the sums */
+        const unsigned lg = (unsigned)((sb.pool_blocks + (uint64_t)kListThreads * kListPerThread - 1) /
+                                       ((uint64_t)kListThreads * kListPerThread));
+        hipError_t e = hipMemsetAsync(sb.tile_blocks, 0, 2 * (FMGI_PRESORT_MAX_TILES + 1) * sizeof(uint32_t), s);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bucket_count, dim3(lg), dim3(kListThreads), 0, s, sb.block_tile, sb.cursor, sb.pool_blocks,
+                           P, sb.tile_blocks);
+        hipLaunchKernelGGL(k_bucket_list, dim3(lg), dim3(kListThreads), 0, s, sb.block_tile, sb.cursor, sb.pool_blocks, P,
+                           sb.tile_blocks, sb.tile_blocks + FMGI_PRESORT_MAX_TILES + 1, sb.block_list);
+        e = fmgi_set_lds_attr_once<3>((const void *)k_bucket_fold, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
-        hipLaunchKernelGGL(k_chain_fold, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
-                           sb.stream, sb.chain_fill, sb.chain_tab, sb.kmax, P, G, (const uint4 *)sb.colpack, lm,
+        hipLaunchKernelGGL(k_bucket_fold, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
+                           sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G, (const uint4 *)sb.colpack, lm,
                            num_texels);
         return hipGetLastError();
     }

@@ -566,7 +566,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
         hipFree(c->sb[k].sorted);
         hipFree(c->sb[k].cursor);
         hipFree(c->sb[k].toff);
-        hipFree(c->sb[k].chain_fill);
+        hipFree(c->sb[k].tile_blocks);
         if (c->ev_baked[k]) hipEventDestroy(c->ev_baked[k]);
         if (c->ev_folded[k]) hipEventDestroy(c->ev_folded[k]);
     }
@@ -639,26 +639,22 @@ static uint64_t stream_cap_for(uint64_t items, int grid, int block) {
 }
 
 /* STREAM layouts (BakeArgs::presort): 0 = unsorted codes, folded through k_slice_sort's sorted copy;
-   1 = ring-sized segments presorted by tile; 2 = per-tile block chains (chain_out / k_chain_fold) */
-enum { kStreamSliced = 0, kStreamSegments = 1, kStreamChains = 2 };
+   1 = ring-sized segments presorted by tile; 2 = per-wave tile buckets (bucket_out / k_bucket_fold) */
+enum { kStreamSliced = 0, kStreamSegments = 1, kStreamBuckets = 2 };
 
-/* the chained stream's pool, in blocks: every code of the chunk, plus each chain's partly filled last block */
-static uint64_t chain_pool_blocks(uint64_t cap, int P) {
-    return (cap + FMGI_CHAIN_BLOCK - 1) / FMGI_CHAIN_BLOCK + (uint64_t)P * FMGI_CHAIN_SHARDS + 8;
+/* the bucketed stream's pool, in blocks: every code of the chunk, plus one partly filled bucket per wave
+   and tile */
+static uint64_t bucket_pool_blocks(uint64_t cap, int P, int grid, int block) {
+    const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
+    return (cap + FMGI_BUCKET_BLOCK - 1) / FMGI_BUCKET_BLOCK + waves * (uint64_t)P + 8;
 }
-/* block positions a chain may hold: 4x its even share (past them, codes go to the lightmap as atomics) */
-static uint32_t chain_kmax(uint64_t cap, int P) {
-    const uint64_t share = ((cap + FMGI_CHAIN_BLOCK - 1) / FMGI_CHAIN_BLOCK + (uint64_t)P * FMGI_CHAIN_SHARDS - 1) /
-                           ((uint64_t)P * FMGI_CHAIN_SHARDS);
-    return (uint32_t)std::min<uint64_t>(4 * share + 16, 0x7FFFFFFFull);
-}
-static uint64_t stream_alloc_codes(uint64_t cap, int P, int mode) {
-    return mode == kStreamChains ? chain_pool_blocks(cap, P) * FMGI_CHAIN_BLOCK : cap;
+static uint64_t stream_alloc_codes(uint64_t cap, int P, int grid, int block, int mode) {
+    return mode == kStreamBuckets ? bucket_pool_blocks(cap, P, grid, block) * FMGI_BUCKET_BLOCK : cap;
 }
 
 static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
-    return stream_alloc_codes(stream_cap_for(items, grid, block), P, mode) > c->sb_cap_alloc[k] ||
+    return stream_alloc_codes(stream_cap_for(items, grid, block), P, grid, block, mode) > c->sb_cap_alloc[k] ||
            (mode == kStreamSliced && !c->sb[k].sorted);
 }
 
@@ -666,7 +662,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     StreamBufs &sb = c->sb[k];
     const uint64_t cap = stream_cap_for(items, grid, block);
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
-    const uint64_t codes = stream_alloc_codes(cap, P, mode);
+    const uint64_t codes = stream_alloc_codes(cap, P, grid, block, mode);
     if (codes > c->sb_cap_alloc[k] || (mode == kStreamSliced && !sb.sorted)) {
         hipFree(sb.stream);
         hipFree(sb.sorted);
@@ -678,13 +674,12 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     }
     sb.presort = mode;
     /* run tables: per 8192-code slice (sorted by k_slice_sort), or per ring-sized segment (presorted); the
-       chained stream's block tables instead */
+       bucketed stream's per-block tile, length and list instead */
     uint64_t entries = 0;
-    if (mode == kStreamChains) {
-        sb.kmax = chain_kmax(cap, P);
-        sb.pool_blocks = chain_pool_blocks(cap, P);
-        entries = (uint64_t)P * FMGI_CHAIN_SHARDS * sb.kmax * 2; /* u32 entries, in u16 units */
-        if (!sb.chain_fill) HIPCHK(hipMalloc(&sb.chain_fill, (size_t)FMGI_MAX_TILES * FMGI_CHAIN_SHARDS * 8));
+    if (mode == kStreamBuckets) {
+        sb.pool_blocks = bucket_pool_blocks(cap, P, grid, block);
+        entries = 3 * sb.pool_blocks * 2; /* three u32 arrays, in u16 units */
+        if (!sb.tile_blocks) HIPCHK(hipMalloc(&sb.tile_blocks, 2 * (FMGI_PRESORT_MAX_TILES + 1) * sizeof(uint32_t)));
     } else {
         const uint64_t nslices = mode == kStreamSegments ? (cap + FMGI_RING_CODES - 1) / FMGI_RING_CODES
                                                          : (cap + FMGI_STREAM_SLICE - 1) / FMGI_STREAM_SLICE;
@@ -697,7 +692,9 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         HIPCHK(hipMalloc(&sb.toff, entries * sizeof(uint16_t)));
         c->sb_entries_alloc[k] = entries;
     }
-    sb.chain_tab = mode == kStreamChains ? (uint32_t *)sb.toff : nullptr;
+    sb.block_tile = mode == kStreamBuckets ? (uint32_t *)sb.toff : nullptr;
+    sb.block_len = mode == kStreamBuckets ? sb.block_tile + sb.pool_blocks : nullptr;
+    sb.block_list = mode == kStreamBuckets ? sb.block_len + sb.pool_blocks : nullptr;
     if (!sb.cursor) HIPCHK(hipMalloc(&sb.cursor, 64));
     sb.cap = cap;
     sb.colpack = c->d_colpack;
@@ -715,9 +712,9 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         if (!(ge && atoi(ge) > 0)) {
             if (mode == kStreamSegments)
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 1024));
-            if (mode == kStreamChains)
+            if (mode == kStreamBuckets) /* at least one 4-KB block per wave of every workgroup */
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
-                                                    std::max<uint64_t>(8, sb.pool_blocks / ((uint64_t)P * 16)));
+                                                    std::max<uint64_t>(8, (cap / FMGI_BUCKET_BLOCK) / ((uint64_t)P * 16)));
         }
         const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
@@ -1113,9 +1110,9 @@ static hipError_t time_end(fmgi_context *c, hipStream_t s, hipEvent_t t0, hipEve
 static uint64_t stream_chunk_items(fmgi_context *c, int sets, int mode) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
-    /* the stream, and the slice-sorted copy of the unsorted layout (chains: the pool is the stream plus one
-       partly filled block per chain, and the block tables, within the 2 % allowance) */
-    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamChains ? 1.02 : 1.0);
+    /* the stream, and the slice-sorted copy of the unsorted layout (buckets: the pool is the stream plus one
+       partly filled block per wave and tile, and the block tables, within the 5 % allowance) */
+    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamBuckets ? 1.05 : 1.0);
     const double held = 4.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]) * (c->sb[0].sorted ? 2.0 : 1.0);
     const double avail = (double)fr + held;
     uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * copies * 4.0 * FMGI_EVENTS_PER_ITEM));
@@ -1394,12 +1391,13 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int lanes = grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block;
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
-    /* the stream layout: per-tile chains (the bake's ring flush sorts by fold tile and appends each tile's
-       run to its chain; the fold reads whole blocks) when the tiles fit one histogram entry per lane, else
-       unsorted codes + k_slice_sort. FMGI_PRESORT=0/1/2 forces unsorted / presorted segments / chains. */
+    /* the stream layout: per-wave tile buckets (the bake's ring flush sorts by fold tile and appends each
+       tile's run to the wave's bucket of that tile; the fold reads whole blocks) when the tiles fit one
+       histogram entry per lane, else unsorted codes + k_slice_sort. FMGI_PRESORT=0/1/2 forces unsorted /
+       presorted segments / buckets. */
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
     const char *pre_env = getenv("FMGI_PRESORT");
-    int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamChains : kStreamSliced;
+    int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamBuckets : kStreamSliced;
     if (pre_env && P >= 1 && P <= FMGI_PRESORT_MAX_TILES) smode = std::max(0, std::min(2, atoi(pre_env)));
     if (pre_env && atoi(pre_env) == 0) smode = kStreamSliced;
     uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, smode);
@@ -1440,14 +1438,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.ntiles = P;
         a.toff = sb.toff;
         a.colpack = (const uint4 *)c->d_colpack;
-        if (smode == kStreamChains) {
-            a.chain_fill = sb.chain_fill;
-            a.chain_tab = sb.chain_tab;
+        if (smode == kStreamBuckets) {
+            a.block_tile = sb.block_tile;
+            a.block_len = sb.block_len;
             a.pool_cursor = sb.cursor;
             a.pool_blocks = sb.pool_blocks;
-            a.kmax = sb.kmax;
-            HIPCHK(hipMemsetAsync(sb.chain_fill, 0, (size_t)P * FMGI_CHAIN_SHARDS * 8, s));
-            HIPCHK(hipMemsetAsync(sb.chain_tab, 0, (size_t)P * FMGI_CHAIN_SHARDS * sb.kmax * 4, s));
         }
         HIPCHK(fetch_table(cb, ce));
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));

@@ -102,17 +102,13 @@ struct BakeArgs {
        in toff[segment * (P + 1) + t]; the fold then needs no sort pass */
     int presort, ntiles;
     uint16_t *toff;
-    /* chained stream (presort == 2, P <= FMGI_PRESORT_MAX_TILES): every ring flush appends each tile's
-       codes to that tile's chain on this workgroup's shard (blockIdx.x & 7): chain c = tile * 8 + shard
-       reserves positions with one atomic (chain_fill[c]) and owns the FMGI_CHAIN_BLOCK-code blocks of the
-       pool listed in chain_tab[c * kmax + k] (block id + 1; 0 = not yet allocated, ~0u = none: its codes
-       went to the lightmap as int64 atomics); the fold reads every tile's blocks as whole 16-KB runs */
-    unsigned long long *chain_fill;
-    uint32_t *chain_tab;
+    /* bucketed stream (presort == 2, P <= FMGI_PRESORT_MAX_TILES): every wave appends each tile's codes
+       to its own open FMGI_BUCKET_BLOCK-code block of the pool (`stream`); blocks are taken with one atomic
+       on pool_cursor, their tile recorded in block_tile[] and their length in block_len[] when they close */
+    uint32_t *block_tile, *block_len;
     unsigned long long *pool_cursor;
     uint64_t pool_blocks;
-    uint32_t kmax;
-    const uint4 *colpack; /* {R, G - R, B - R, 0} per colour state (the chain path's rare atomic fallback) */
+    const uint4 *colpack; /* {R, G - R, B - R, 0} per colour state (the bucketed stream's atomic fallback) */
     int ring_off;                 /* byte offset of the per-wave code rings in dynamic LDS (fmgi_bake_lds) */
     int num_texels;
     /* debug trace (TRACE kernels only) */
@@ -130,10 +126,10 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 static_assert(FMGI_STREAM_BLOCK % FMGI_RING_CODES == 0, "ring flushes must tile the stream blocks");
 #define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
 #define FMGI_RING_STRIDE (FMGI_RING_CODES + 384) /* per-wave LDS: ring, its overflow (64), tile histogram (64),
-                                                    the chained stream's per-tile info (64 x 16 B) */
+                                                    the bucketed stream's per-tile info (64 x 16 B) */
 #define FMGI_PRESORT_MAX_TILES 63 /* presorted stream: a tile histogram of one entry per lane        */
-#define FMGI_CHAIN_BLOCK 4096  /* codes per block of a tile chain (16 KB)                      */
-#define FMGI_CHAIN_SHARDS 8    /* chains per tile (workgroup shards): spreads the reservation atomics */
+#define FMGI_BUCKET_BLOCK 1024 /* codes per block of the bucketed stream (4 KB; >= a ring, so a ring's run of
+                                  one tile spans at most two blocks)                              */
 #define FMGI_TILE_BITS 11      /* 2048-texel tiles summed in LDS (64 KB: two sum workgroups per
                                   CU; measured 25 ms per 1e9 photons vs 28 ms with 4096, 31 ms with 1024) */
 #define FMGI_MAX_TILES 2048    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */
@@ -150,10 +146,10 @@ struct StreamBufs {
     int presort;                /* codes were written presorted per FMGI_RING_CODES segment (toff per
                                    segment); the fold skips k_slice_sort                         */
     int block;                  /* threads per sum workgroup (256, 512 or 1024)                  */
-    /* chained stream (presort == 2): the pool is `stream` (pool_blocks x FMGI_CHAIN_BLOCK codes) */
-    unsigned long long *chain_fill; /* [P * FMGI_CHAIN_SHARDS] codes reserved per chain             */
-    uint32_t *chain_tab;            /* [P * FMGI_CHAIN_SHARDS * kmax] block id + 1 per chain position */
-    uint32_t kmax;
+    /* bucketed stream (presort == 2): the pool is `stream` (pool_blocks x FMGI_BUCKET_BLOCK codes) */
+    uint32_t *block_tile, *block_len; /* [pool_blocks] per block: its tile, its length              */
+    uint32_t *block_list;             /* [pool_blocks] block ids grouped by tile (the fold's list)     */
+    uint32_t *tile_blocks;            /* [2 * (FMGI_PRESORT_MAX_TILES + 1)] counts, then list cursors  */
     uint64_t pool_blocks;
 };
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);

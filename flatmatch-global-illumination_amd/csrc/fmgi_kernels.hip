@@ -908,47 +908,36 @@ struct AccStream {
         ws.base += FMGI_RING_CODES;
     }
 
-    /* ---- chained stream (BakeArgs::presort == 2) ---- */
+    /* ---- bucketed stream (BakeArgs::presort == 2) ----
+       Every wave keeps, per fold tile, one open FMGI_BUCKET_BLOCK-code block of the pool (its private
+       bucket: no other wave writes it). A ring flush sorts the ring by tile and appends each tile's run to
+       the wave's bucket of that tile; a bucket that fills is closed (its length recorded) and a fresh block
+       is taken with one atomic on the pool cursor, the block's tile recorded beside it. The fold lists the
+       blocks by tile and reads them as whole 4-KB runs. Per-wave state, in the wave's LDS info table:
+       info[t] = {open block (kNoBlock: none), codes in it, (flush temporaries)}. */
     static constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+    static constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
 
-    /* the pool block of position k of chain c: allocated by the one reservation whose range holds the
-       block's first position (chain_reserve), published with an agent-scope store; a reader polls until
-       it appears (the allocating lane never waits before publishing, so the poll ends) */
-    static __device__ __forceinline__ uint32_t chain_block(const BakeArgs &a, uint32_t c, uint64_t k) {
-        if (k >= a.kmax) return kNoBlock;
-        uint32_t *slot = a.chain_tab + (uint64_t)c * a.kmax + k;
-        for (int it = 0; it < (1 << 22); it++) {
-            const uint32_t v = __hip_atomic_load(slot, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            if (v) return v == kNoBlock ? kNoBlock : v - 1;
-            __builtin_amdgcn_s_sleep(1);
-        }
-        atomicAdd(a.overflow, 1ull); /* never (bounded wait): the call fails instead of hanging */
-        return kNoBlock;
+    static __device__ __forceinline__ uint4 *bucket_info(uint32_t *ring) {
+        return (uint4 *)(ring + FMGI_RING_CODES + 128);
     }
-    static __device__ __forceinline__ uint32_t chain_alloc(const BakeArgs &a, uint32_t c, uint64_t k) {
-        if (k >= a.kmax) return kNoBlock;
+    /* at the start of the bake: no wave has an open bucket */
+    static __device__ __forceinline__ void bucket_init(const BakeArgs &a, uint32_t *ring) {
+        uint4 *info = bucket_info(ring);
+        for (int t = (int)__lane_id(); t < 64; t += 64) info[t] = make_uint4(kNoBlock, BP, 0u, kNoBlock);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+    /* a fresh pool block for tile t (kNoBlock if the pool is exhausted: never, by sizing) */
+    static __device__ __forceinline__ uint32_t bucket_alloc(const BakeArgs &a, uint32_t t) {
         const unsigned long long b = atomicAdd(a.pool_cursor, 1ull);
-        const uint32_t v = b < a.pool_blocks ? (uint32_t)b + 1 : kNoBlock;
-        __hip_atomic_store(a.chain_tab + (uint64_t)c * a.kmax + k, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-        return v == kNoBlock ? kNoBlock : (uint32_t)b;
+        if (b >= a.pool_blocks) return kNoBlock;
+        a.block_tile[b] = t;
+        return (uint32_t)b;
     }
-    /* n codes of chain c reserved at positions [p, p + n) (n <= FMGI_RING_CODES < FMGI_CHAIN_BLOCK, so at
-       most two blocks): allocates the block whose first position it holds, returns both blocks */
-    static __device__ __forceinline__ void chain_reserve(const BakeArgs &a, uint32_t c, uint64_t p, uint32_t n,
-                                                         uint32_t &b0, uint32_t &b1) {
-        constexpr uint64_t B = FMGI_CHAIN_BLOCK;
-        const uint64_t k0 = p / B, k1 = (p + n - 1) / B;
-        uint32_t mine = kNoBlock;
-        uint64_t km = ~0ull;
-        if (p % B == 0) km = k0;
-        else if (k1 > k0) km = k1;
-        if (km != ~0ull) mine = chain_alloc(a, c, km);
-        b0 = km == k0 ? mine : chain_block(a, c, k0);
-        b1 = k1 == k0 ? b0 : (km == k1 ? mine : chain_block(a, c, k1));
-    }
-    /* the rare fallback (a chain past kmax blocks, or the pool exhausted): the code's colour, added to
-       the int64 lightmap with device atomics (exact, order-free, as AccFx3) */
-    static __device__ __forceinline__ void chain_atomic(const BakeArgs &a, uint32_t code) {
+    /* the fallback of an exhausted pool: the code's colour, added to the int64 lightmap with device
+       atomics (exact, order-free, as AccFx3) */
+    static __device__ __forceinline__ void bucket_atomic(const BakeArgs &a, uint32_t code) {
         const uint4 cc = a.colpack[code & 1023];
         unsigned long long *q = a.lm + 4 * (size_t)(code >> 10);
         const unsigned long long r = cc.x;
@@ -957,52 +946,141 @@ struct AccStream {
         atomicAdd(q + 2, r + (unsigned long long)(long long)(int32_t)cc.z);
     }
 
-    /* chained stream: append ring[0, n) to the tiles' chains. An LDS histogram counts the codes per tile;
-       one lane per tile reserves its run in its chain with one atomic and resolves the run's blocks into
-       the wave's info table; every code then takes a rank in its run (a returning LDS add on the reset
-       histogram) and is stored at its position. Codes stay in the ring (no registers held across the
-       reservation). Called where every live lane of the wave is active. */
-    static __device__ __forceinline__ void chain_out(const BakeArgs &a, uint32_t *ring, uint32_t n) {
-        constexpr uint32_t B = FMGI_CHAIN_BLOCK;
+    /* place tile t's run of cnt codes (ring run start `start`) in the wave's bucket: info[t] becomes
+       {first block, offset in it, run start, second block} (the second only when the bucket fills up) */
+    static __device__ __forceinline__ void bucket_place(const BakeArgs &a, uint4 *info, int t, uint32_t start,
+                                                        uint32_t cnt) {
+        const uint4 st = info[t];
+        const uint32_t room = BP - st.y; /* 0 without an open bucket (y = BP) */
+        uint32_t second = kNoBlock;
+        if (cnt <= room) {
+            if (cnt == room && st.x != kNoBlock) a.block_len[st.x] = BP;
+        } else {
+            if (room && st.x != kNoBlock) a.block_len[st.x] = BP;
+            second = bucket_alloc(a, (uint32_t)t);
+            if (cnt - room == BP && second != kNoBlock) a.block_len[second] = BP;
+        }
+        info[t] = make_uint4(st.x, st.y, start, second);
+    }
+    /* the code of rank rk in tile t's run goes to ... (info as bucket_place left it) */
+    static __device__ __forceinline__ void bucket_store(const BakeArgs &a, uint4 inf, uint32_t rk, uint32_t code) {
+        const uint32_t room = BP - inf.y;
+        const bool first = rk < room;
+        const uint32_t blk = first ? inf.x : inf.w;
+        if (blk == kNoBlock) bucket_atomic(a, code);
+        else a.stream[(uint64_t)blk * BP + (first ? inf.y + rk : rk - room)] = code;
+    }
+    /* ... and the bucket after the run: the first block while the run fit in it, else the second */
+    static __device__ __forceinline__ void bucket_advance(uint4 *info, int t, uint32_t cnt) {
+        const uint4 inf = info[t];
+        const uint32_t room = BP - inf.y;
+        info[t] = cnt <= room ? make_uint4(inf.x, inf.y + cnt, 0u, kNoBlock) : make_uint4(inf.w, cnt - room, 0u, kNoBlock);
+    }
+
+    /* bucketed stream: append ring[0, n) to the wave's tile buckets. With every lane live (the common
+       case), each lane holds 16 codes while an LDS histogram counts them per tile, a scan gives each tile's
+       run start, and the codes are scattered back into the ring sorted by tile; the lane of tile t places
+       the run in its bucket (bucket_place), and the lanes store the sorted ring, consecutive lanes to
+       consecutive positions of one run. With lanes already done (the bake's tail) the ring is not sorted:
+       each code takes its rank in its run from a second pass over the histogram. Called where every live
+       lane of the wave is active. */
+    static __device__ __forceinline__ void bucket_out(const BakeArgs &a, uint32_t *ring, uint32_t n) {
         uint32_t *hist = ring + FMGI_RING_CODES + 64;
-        uint4 *info = (uint4 *)(hist + 64); /* per tile {block 0, offset in it, codes that fit in it, block 1} */
+        uint4 *info = bucket_info(ring);
         const uint64_t live = __ballot(true);
         const uint32_t nl = (uint32_t)__popcll(live);
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
         const int P = a.ntiles;
-        const uint32_t shift = 10 + FMGI_TILE_BITS, shard = blockIdx.x & (FMGI_CHAIN_SHARDS - 1);
+        const uint32_t shift = 10 + FMGI_TILE_BITS;
         for (uint32_t t = r; t < 64; t += nl) hist[t] = 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        for (int t = (int)r; t < P; t += (int)nl) {
-            const uint32_t cnt = hist[t];
-            uint4 inf = make_uint4(kNoBlock, 0u, 0u, kNoBlock);
-            if (cnt) {
-                const uint32_t c = (uint32_t)t * FMGI_CHAIN_SHARDS + shard;
-                const uint64_t p = atomicAdd(a.chain_fill + c, (unsigned long long)cnt);
-                uint32_t k0b, k1b;
-                chain_reserve(a, c, p, cnt, k0b, k1b);
-                inf = make_uint4(k0b, (uint32_t)(p % B), B - (uint32_t)(p % B), k1b);
+        if (nl == 64) {
+            uint32_t cr[16];
+            if (n == FMGI_RING_CODES) {
+                const uint4 *rq = (const uint4 *)ring + 4 * r;
+#pragma unroll
+                for (int h = 0; h < 4; h++) {
+                    const uint4 c = rq[h];
+                    cr[4 * h] = c.x, cr[4 * h + 1] = c.y, cr[4 * h + 2] = c.z, cr[4 * h + 3] = c.w;
+                }
+            } else {
+#pragma unroll
+                for (int e = 0; e < 16; e++) cr[e] = 16 * r + e < n ? ring[16 * r + e] : 0xFFFFFFFFu;
             }
-            info[t] = inf;
-            hist[t] = 0; /* the run's rank cursor from here on */
+#pragma unroll
+            for (int e = 0; e < 16; e++)
+                if (cr[e] != 0xFFFFFFFFu) atomicAdd(&hist[cr[e] >> shift], 1u);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const uint32_t cnt = (int)r < P ? hist[r] : 0u; /* lane t: tile t */
+            uint32_t incl = cnt;
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = __shfl_up(incl, off, 64);
+                if ((int)r >= off) incl += o;
+            }
+            const uint32_t start = incl - cnt;
+            if ((int)r < P) hist[r] = start;
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll
+            for (int h = 0; h < 16; h += 8) {
+                uint32_t o[8];
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                    o[e] = cr[h + e] != 0xFFFFFFFFu ? atomicAdd(&hist[cr[h + e] >> shift], 1u) : 0u;
+#pragma unroll
+                for (int e = 0; e < 8; e++)
+                    if (cr[h + e] != 0xFFFFFFFFu) ring[o[e]] = cr[h + e];
+            }
+            if ((int)r < P && cnt) bucket_place(a, info, (int)r, start, cnt);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+#pragma unroll 4
+            for (uint32_t i = r; i < n; i += 64) {
+                const uint32_t code = ring[i];
+                const uint4 inf = info[code >> shift];
+                bucket_store(a, inf, i - inf.z, code);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if ((int)r < P && cnt) bucket_advance(info, (int)r, cnt);
+        } else {
+            for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int t = (int)r; t < P; t += (int)nl) {
+                const uint32_t cnt = hist[t];
+                if (cnt) bucket_place(a, info, t, 0u, cnt);
+                hist[t + 64 * 0] = cnt;
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            /* ranks: a second count, from the top (hist[t] counts down to 0) */
+            for (uint32_t k = r; k < n; k += nl) {
+                const uint32_t code = ring[k], t = code >> shift;
+                const uint32_t rk = atomicSub(&hist[t], 1u) - 1u;
+                bucket_store(a, info[t], rk, code);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            /* the run lengths again (hist is 0 now): from the codes' tiles */
+            for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            for (int t = (int)r; t < P; t += (int)nl)
+                if (hist[t]) bucket_advance(info, t, hist[t]);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        for (uint32_t k = r; k < n; k += nl) {
-            const uint32_t code = ring[k], t = code >> shift;
-            const uint32_t rk = atomicAdd(&hist[t], 1u);
+    }
+    /* at the end of the bake: the open buckets' lengths */
+    static __device__ __forceinline__ void bucket_close(const BakeArgs &a, uint32_t *ring) {
+        const uint4 *info = bucket_info(ring);
+        for (int t = (int)__lane_id(); t < a.ntiles; t += 64) {
             const uint4 inf = info[t];
-            const bool first = rk < inf.z;
-            const uint32_t blk = first ? inf.x : inf.w;
-            if (blk == kNoBlock) chain_atomic(a, code);
-            else a.stream[(uint64_t)blk * B + (first ? inf.y + rk : rk - inf.z)] = code;
+            if (inf.x != kNoBlock && inf.y < BP) a.block_len[inf.x] = inf.y;
         }
-        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-        __builtin_amdgcn_wave_barrier();
     }
 
     static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, uint32_t *ring, bool dep,
@@ -1016,7 +1094,7 @@ struct AccStream {
         ws.tot += n;
         if (fill + n < FMGI_RING_CODES) return;
         /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
-        if (a.presort == 2) chain_out(a, ring, FMGI_RING_CODES);
+        if (a.presort == 2) bucket_out(a, ring, FMGI_RING_CODES);
         else if (a.presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
         else copy_out(a, ws, ring, FMGI_RING_CODES);
         const uint32_t rest = fill + n - FMGI_RING_CODES; /* < n <= live lanes: one code per live lane */
@@ -1041,8 +1119,9 @@ struct AccStream {
         ws.end = __shfl(ws.end, src, 64);
         const uint32_t fill = ws.tot % FMGI_RING_CODES, padded = (fill + 3) & ~3u;
         const uint32_t lane = __lane_id();
-        if (a.presort == 2) { /* the last (partial) ring into the chains */
-            if (fill) chain_out(a, ring, fill);
+        if (a.presort == 2) { /* the last (partial) ring into the buckets, then close them */
+            if (fill) bucket_out(a, ring, fill);
+            bucket_close(a, ring);
             return;
         }
         if (a.presort) { /* the last (partial) ring, then empty run tables for the block's unused segments */
@@ -1134,6 +1213,8 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
         __syncthreads();
     }
+    if constexpr (HasAppend<Acc>::value)
+        if (a.presort == 2) AccStream::bucket_init(a, ring);
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
