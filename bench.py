@@ -42,12 +42,14 @@ HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
 
 
 def valu_peak():
-    """Measured wave64 VALU issue ceiling of one MI355X (tools/valu_peak.hip -> profiles/valu_peak.json)."""
+    """Measured wave64 VALU issue ceiling of one MI355X per SIMD-cycle at the measured in-kernel clock
+    (tools/valu_peak.hip, >= 50 ms launches -> profiles/valu_peak.json), by resident waves per SIMD."""
     p = os.path.join(REPO, "profiles", "valu_peak.json")
     try:
-        return float(json.load(open(p))["peak_wave_valu_insts_per_s"])
+        d = json.load(open(p))
+        return {int(k): float(v) for k, v in d["f32_per_simd_per_clk_by_waves"].items()}, d.get("source", p)
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 def load_scene(name):
@@ -150,15 +152,89 @@ def pmc_traffic(config_name):
     return d.get("hbm_bytes_per_launch") if "k_bake" in d.get("kernel", "") else None
 
 
-def sq_counters(config_name):
-    """Per-launch SQ counters of the bake from the committed rocprofv3 summary (profiles/sq_issue.json)."""
+def sq_record(config_name):
+    """Per-launch counters of the bake (SQ, GRBM, TA/TD/TCP) and its measured clock, from the committed
+    summary of one session's rocprofv3 --pmc passes (profiles/sq_issue.json, tools/sq_summary.py)."""
     p = os.path.join(REPO, "profiles", "sq_issue.json")
     if not os.path.exists(p):
         return None
     try:
-        return json.load(open(p)).get(config_name, {}).get("per_launch")
+        return json.load(open(p)).get(config_name)
     except (OSError, ValueError):
         return None
+
+
+def issue_block(rec, ks, per_launch_scans, cus):
+    """The bake's bounded issue and memory-path figures. Every fraction is <= 1 by construction:
+      SIMD cycles   = GRBM_GUI_ACTIVE / 8 XCDs x 4 SIMDs x CUs (the profiled launch's own busy cycles;
+                      the live launch time x the in-kernel clock is given beside it)
+      VALU / total instructions per SIMD-cycle, against the measured VALU ceiling at the same occupancy
+      wave-cycle split: SQ_ACTIVE_INST_ANY (issuing) + SQ_WAIT_INST_ANY (ready, issue-stalled) +
+                      SQ_WAIT_ANY (parked on s_waitcnt / barrier) = SQ_WAVE_CYCLES (MI355X_MICROARCH.md)
+      TA / TD busy  = TA_TA_BUSY_sum, TD_TD_BUSY_sum over (CUs x the per-XCD busy cycles)"""
+    per = rec.get("per_launch", {})
+    need = ("SQ_INSTS_VALU", "SQ_WAVE_CYCLES", "SQ_WAIT_ANY", "SQ_ACTIVE_INST_ANY", "SQ_WAIT_INST_ANY",
+            "GRBM_GUI_ACTIVE", "SQ_WAVES")
+    if not all(per.get(k) for k in need):
+        return None
+    cyc = per["GRBM_GUI_ACTIVE"] / 8.0
+    simd_cycles = cyc * 4.0 * cus
+    insts = {k: per.get(f"SQ_INSTS_{k}", 0.0) for k in ("VALU", "SALU", "SMEM", "BRANCH", "VMEM", "LDS")}
+    total = sum(insts.values())
+    waves_per_simd = per["SQ_WAVES"] / (4.0 * cus)
+    peaks, peak_src = valu_peak()
+    vpeak = None
+    if peaks:
+        w = max(1, int(round(waves_per_simd)))
+        vpeak = peaks.get(w) or peaks[min(peaks, key=lambda k: abs(k - w))]
+    wc = per["SQ_WAVE_CYCLES"]
+    clock = rec.get("clock_ghz")
+    vpc = insts["VALU"] / simd_cycles
+    out = {
+        "clock_ghz": clock,
+        "clock_source": rec.get("clock_source"),
+        "profiled_launch_ms": cyc / (clock * 1e6) if clock else None,
+        "simd_cycles_per_launch": simd_cycles,
+        "live_simd_cycles_per_launch": ks * clock * 1e9 * 4.0 * cus if clock else None,
+        "waves_per_simd": waves_per_simd,
+        "valu_per_simd_cycle": vpc,
+        "insts_per_simd_cycle": total / simd_cycles,
+        "valu_peak_per_simd_cycle": vpeak,
+        "valu_frac_of_peak": vpc / vpeak if vpeak else None,
+        "wave_cycles": {"issuing": per["SQ_ACTIVE_INST_ANY"] / wc, "issue_stalled": per["SQ_WAIT_INST_ANY"] / wc,
+                        "waiting": per["SQ_WAIT_ANY"] / wc},
+        "insts_per_launch": insts,
+        "insts_per_scan_wave": {k: 64.0 * v / per_launch_scans for k, v in insts.items()},
+        "source": f"{rec.get('source')}; VALU ceiling {peak_src}",
+    }
+    if per.get("TA_TA_BUSY_sum"):
+        out["vmem_path"] = {
+            "ta_busy": per["TA_TA_BUSY_sum"] / (cus * cyc),
+            "td_busy": per.get("TD_TD_BUSY_sum", 0.0) / (cus * cyc),
+            "td_stalled_on_tc": per.get("TD_TC_STALL_sum", 0.0) / (cus * cyc),
+            "tcp_accesses_per_scan_wave": 64.0 * per.get("TCP_TOTAL_CACHE_ACCESSES_sum", 0.0) / per_launch_scans,
+        }
+    return out
+
+
+def binding_of(issue, atomic_rate):
+    """(roofline.bound, binding) from the measured figures: the resource closest to saturation"""
+    if atomic_rate > 0.8 * 2.0e10:
+        return "atomics", "memory-side atomic rate"
+    if not issue:
+        return "latency", "unmeasured for this config (no committed counter summary): see DESIGN.md §4.1"
+    vm = issue.get("vmem_path", {})
+    fr = {"vmem": max(vm.get("ta_busy", 0.0), vm.get("td_busy", 0.0)),
+          "valu": issue.get("valu_frac_of_peak") or 0.0}
+    res = max(fr, key=fr.get)
+    w = issue["wave_cycles"]
+    if fr[res] >= 0.85:
+        what = {"vmem": "vector-memory path (TA/TD busy %.0f %% of cycles)" % (100 * fr["vmem"]),
+                "valu": "VALU issue (%.0f %% of the measured ceiling)" % (100 * fr["valu"])}[res]
+        return res, what + "; waves parked on s_waitcnt %.0f %% of wave cycles" % (100 * w["waiting"])
+    return "latency", ("dependent-load latency: waves parked on s_waitcnt %.0f %% of wave cycles, issuing %.0f %%; "
+                       "VALU %.0f %% of its ceiling, TA/TD busy %.0f %%"
+                       % (100 * w["waiting"], 100 * w["issuing"], 100 * fr["valu"], 100 * fr["vmem"]))
 
 
 def main():
@@ -196,6 +272,15 @@ def main():
             dist.init_process_group("nccl", device_id=torch.device("cuda", local))
         else:
             dist.init_process_group(backend)
+
+    # what the job ran on: torch.distributed's world, and the ranks RCCL itself counts (an all-reduce of
+    # ones over the process group's communicator)
+    dist_info = {"world_size": dist.get_world_size() if world > 1 else 1, "backend": backend if world > 1 else None,
+                 "rccl_ranks": None}
+    if world > 1 and backend == "nccl":
+        one = torch.ones(1, dtype=torch.int32, device=torch.device("cuda", device_index))
+        dist.all_reduce(one)
+        dist_info["rccl_ranks"] = int(one.item())
 
     cfg = dict(CONFIGS[args.config])
     if args.spa:
@@ -295,26 +380,12 @@ def main():
         atomic_rate = per_dep * per_launch_deps / ks
         atomics = {"per_deposit": per_dep, "achieved_per_s": atomic_rate, "ceiling_per_s": 2.0e10,
                    "frac": atomic_rate / 2.0e10}
-        # the bake's own ceiling: instruction issue. SQ counters of this config (profiles/sq_issue.json,
-        # rocprofv3 --pmc) over the live HIP-event kernel time, against the measured VALU ceiling
-        # (profiles/valu_peak.json); SQ_ACTIVE_INST_ANY / SQ_WAVE_CYCLES x waves per SIMD is the share of
-        # SIMD time some wave of it issues an instruction (any type)
-        sq = sq_counters(args.config) or {}
-        vpeak = valu_peak()
-        issue = None
-        if sq.get("SQ_INSTS_VALU") and vpeak:
-            waves_per_simd = sq["SQ_WAVES"] / (4.0 * torch.cuda.get_device_properties(dev).multi_processor_count)
-            insts = {k: sq.get(f"SQ_INSTS_{k}", 0.0) for k in ("VALU", "SALU", "BRANCH", "VMEM_RD", "LDS")}
-            issue = {"achieved": sq["SQ_INSTS_VALU"] / ks, "peak": vpeak, "unit": "wave-VALU-instr/s",
-                     "frac": sq["SQ_INSTS_VALU"] / ks / vpeak,
-                     "issue_busy_frac": sq["SQ_ACTIVE_INST_ANY"] / sq["SQ_WAVE_CYCLES"] * waves_per_simd,
-                     "valu_busy_frac": sq["SQ_ACTIVE_INST_VALU"] / sq["SQ_WAVE_CYCLES"] * waves_per_simd,
-                     "waves_per_simd": waves_per_simd,
-                     "insts_per_launch": insts,
-                     "insts_per_scan_wave": {k: 64.0 * v / per_launch_scans for k, v in insts.items()},
-                     "source": "profiles/sq_issue.json (rocprofv3 --pmc SQ_*), profiles/valu_peak.json (tools/valu_peak)"}
-        binding = ("memory-side atomic rate" if atomic_rate > 0.8 * 2.0e10 else
-                   "instruction issue and latency of the per-lane scan/bounce loop (not HBM: see issue)")
+        # what binds the bake: counters of this config and build (profiles/sq_issue.json) against the
+        # measured clock and VALU ceiling; bounded fractions only (issue_block)
+        rec = sq_record(args.config)
+        issue = issue_block(rec, ks, per_launch_scans, torch.cuda.get_device_properties(dev).multi_processor_count) \
+            if rec else None
+        bound, binding = binding_of(issue, atomic_rate)
         out = {
             "metric": METRIC,
             "value": value,
@@ -342,11 +413,13 @@ def main():
                 "parallelism": f"dp{world} (work-item shards, RCCL reduce of int64 lightmaps)" if backend == "nccl"
                 else f"dp{world} REHEARSAL ({backend}: ranks share {torch.cuda.device_count()} GPU(s), host reduce)",
             },
+            "distributed": dist_info,
             "roofline": {
                 # BASELINE metric: achieved HBM GB/s of the dominant kernel (the bake) as a fraction of the
                 # HBM peak, algorithmic bytes per SURVEY.md §8d (12 B per deposit) / HIP-event kernel time.
-                # The bake is not HBM-bound (it writes 4 B per deposit); `binding` and `issue` say what is.
-                "bound": "hbm",
+                # The bake is not HBM-bound (it writes 4 B per deposit): `bound` names the resource the
+                # counters show closest to saturation, `binding` and `issue` the figures.
+                "bound": bound,
                 "achieved": achieved_gbs,
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",

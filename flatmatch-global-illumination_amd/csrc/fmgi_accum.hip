@@ -343,8 +343,8 @@ __global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict
             const uint32_t cs[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                if (i0 + m >= len) continue;
                 const uint32_t c = cs[m];
+                if (i0 + m >= len || c == kSentinel) continue; /* runs are padded to 4 codes */
                 const int tx = (int)((c >> 10) & (kTileTexels - 1));
                 const uint4 cc = col[c & 1023];
                 atomicAdd(&acc_r[tx], (unsigned long long)cc.x);

@@ -644,9 +644,12 @@ enum { kStreamSliced = 0, kStreamSegments = 1, kStreamBuckets = 2 };
 
 /* the bucketed stream's pool, in blocks: every code of the chunk, plus one partly filled bucket per wave
    and tile */
+/* pool blocks for `cap` codes: the codes, the sentinel pads (<= 3 per tile and ring flush: a flush per
+   FMGI_RING_CODES codes plus each wave's last), and one partly filled block per wave and tile */
 static uint64_t bucket_pool_blocks(uint64_t cap, int P, int grid, int block) {
     const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
-    return (cap + FMGI_BUCKET_BLOCK - 1) / FMGI_BUCKET_BLOCK + waves * (uint64_t)P + 8;
+    const uint64_t pads = (cap / FMGI_RING_CODES + waves) * 3u * (uint64_t)P;
+    return (cap + pads + FMGI_BUCKET_BLOCK - 1) / FMGI_BUCKET_BLOCK + waves * (uint64_t)P + 8;
 }
 static uint64_t stream_alloc_codes(uint64_t cap, int P, int grid, int block, int mode) {
     return mode == kStreamBuckets ? bucket_pool_blocks(cap, P, grid, block) * FMGI_BUCKET_BLOCK : cap;
@@ -1023,6 +1026,15 @@ static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs,
     return off;
 }
 
+/* the kernel instance a bake of `kernel` launches: the grid scan of a closed box (one plane per axis and
+   class) has its own instance (FMGI_KVAR_AXES); FMGI_NO_AXES (experiments) keeps the general one */
+static bool grid_axes_scene(const fmgi_context *c) {
+    return c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES");
+}
+static int kernel_instance(const fmgi_context *c, int kernel) {
+    return kernel == FMGI_KERNEL_GRID && grid_axes_scene(c) ? (kernel | FMGI_KVAR_AXES) : kernel;
+}
+
 static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool trace) {
     StagePlan p;
     const char *be = getenv("FMGI_BLOCK");
@@ -1032,7 +1044,7 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     const char *se = getenv("FMGI_SRCS_LDS"), *re = getenv("FMGI_RECTS_LDS");
     const bool srcs = c->nsrcs > 0 && !(se && atoi(se) == 0);
     const int rects_mode = re ? atoi(re) : -1; /* -1 auto */
-    const int kfn = kernel == FMGI_KERNEL_FAST && false ? kernel : kernel;
+    const int kfn = kernel_instance(c, kernel);
     /* resident waves per CU of a (block, staged bytes) choice; 0 if it cannot launch */
     auto waves = [&](int block, int bytes) -> int {
         if (fmgi_bake_lds(kfn, accum, block, bytes, nullptr) > kBakeLdsMax) return 0;
@@ -1070,7 +1082,7 @@ static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace,
     /* persistent grid: exactly the blocks that are resident at once (occupancy from the VGPR/SGPR/LDS
        use of the kernel actually launched), so no block starts late and lengthens the tail; never more
        lanes than work items */
-    int per_cu = fmgi_bake_resident_blocks(kernel, accum, trace, block, lds);
+    int per_cu = fmgi_bake_resident_blocks(kernel_instance(c, kernel), accum, trace, block, lds);
     if (per_cu <= 0) per_cu = 4;
     if (const char *pe = getenv("FMGI_BAKE_WG_PER_CU")) /* experiments: leave room for concurrent folds */
         if (atoi(pe) > 0) per_cu = std::min(per_cu, atoi(pe));
@@ -1110,9 +1122,10 @@ static hipError_t time_end(fmgi_context *c, hipStream_t s, hipEvent_t t0, hipEve
 static uint64_t stream_chunk_items(fmgi_context *c, int sets, int mode) {
     size_t fr = 0, tot = 0;
     if (hipMemGetInfo(&fr, &tot) != hipSuccess) fr = (size_t)8 << 30;
-    /* the stream, and the slice-sorted copy of the unsorted layout (buckets: the pool is the stream plus one
-       partly filled block per wave and tile, and the block tables, within the 5 % allowance) */
-    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamBuckets ? 1.05 : 1.0);
+    /* the stream, and the slice-sorted copy of the unsorted layout (buckets: the pool is the stream plus its
+       pads (<= 3 * 63 per 1024 codes), one partly filled block per wave and tile, and the block tables,
+       within the 25 % allowance) */
+    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamBuckets ? 1.25 : 1.0);
     const double held = 4.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]) * (c->sb[0].sorted ? 2.0 : 1.0);
     const double avail = (double)fr + held;
     uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * copies * 4.0 * FMGI_EVENTS_PER_ITEM));
@@ -1174,7 +1187,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.gcells = c->d_gcells;
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
-        a.grid_axes = (c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES")) ? 1 : 0;
+        a.grid_axes = grid_axes_scene(c) ? 1 : 0;
         a.grid_xy_separate = getenv("FMGI_GRID_SEPARATE") ? 1 : 0;
     } else if (kernel == FMGI_KERNEL_HYBRID) {
         a.fimg = c->d_himg;
@@ -1370,7 +1383,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace,
+        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), c->accum, trace,
                                 grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop),
                                 block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
@@ -1449,7 +1462,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel, c->accum, trace, grid, block, s));
+        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), c->accum, trace, grid, block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         if (overlap) {
             HIPCHK(hipEventRecord(c->ev_baked[k], s));

@@ -125,8 +125,11 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 #define FMGI_RING_CODES 1024   /* codes a wave collects in LDS before writing them out       */
 static_assert(FMGI_STREAM_BLOCK % FMGI_RING_CODES == 0, "ring flushes must tile the stream blocks");
 #define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
-#define FMGI_RING_STRIDE (FMGI_RING_CODES + 384) /* per-wave LDS: ring, its overflow (64), tile histogram (64),
-                                                    the bucketed stream's per-tile info (64 x 16 B) */
+#define FMGI_RING_PAD 192 /* the ring's overflow (< 64 codes) lies in the first 64 of these; the bucketed
+                             stream sorts a flush into ring[0, RING + 3 * 63) (runs padded to 4 codes)   */
+#define FMGI_RING_HIST (FMGI_RING_CODES + FMGI_RING_PAD)      /* tile histogram (64)                     */
+#define FMGI_RING_INFO (FMGI_RING_HIST + 64)                  /* bucketed stream's per-tile info (64 x 16 B) */
+#define FMGI_RING_STRIDE (FMGI_RING_INFO + 256)               /* per-wave LDS dwords                     */
 #define FMGI_PRESORT_MAX_TILES 63 /* presorted stream: a tile histogram of one entry per lane        */
 #define FMGI_BUCKET_BLOCK 1024 /* codes per block of the bucketed stream (4 KB; >= a ring, so a ring's run of
                                   one tile spans at most two blocks)                              */
@@ -160,6 +163,9 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
 #define FMGI_KERNEL_FAST_COOP 101
 
 /* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only), 4 = AccStream */
+/* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
+   FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */
+#define FMGI_KVAR_AXES 0x100
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);

@@ -603,10 +603,14 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
     }
 }
 
-struct ScanGrid {
+/* Axes = true: the closed-box specialisation (one plane per axis and class, BakeArgs::grid_axes), whose
+   kernel holds grid_phase1_axes alone: the general kernel's register and SGPR budget is set by its layout
+   walks, and its spilled SGPRs come back as v_readlane in the box scan too */
+template <bool Axes>
+struct ScanGridT {
     static constexpr bool kLds = true;
     static constexpr bool kCoop = false;
-    static constexpr int kMinWaves = 5; /* k_bake occupancy floor for the register allocator */
+    static constexpr int kMinWaves = 4; /* k_bake occupancy floor for the register allocator */
     static constexpr int kOrderedRounds = 12;
 
     /*
@@ -647,7 +651,7 @@ struct ScanGrid {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         unsigned ntest = 0;
-        if (a.grid_axes) {
+        if (Axes) {
             grid_phase1_axes(a, lds, src, dir, L1, L2, code1, ntest);
         } else if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
             grid_phase1_sorted(a, lds, src, dir, L1, L2, code1, ntest);
@@ -695,6 +699,9 @@ struct ScanGrid {
         st.clk.lap(ST_FALLBACK);
     }
 };
+
+using ScanGrid = ScanGridT<false>;
+using ScanGridAxes = ScanGridT<true>;
 
 /*
  * ScanHybrid: the reference's apartment layouts have few floor/ceiling planes holding many records
@@ -834,7 +841,7 @@ struct AccStream {
                                                       uint32_t n) {
         if (ws.end - ws.base < FMGI_RING_CODES) reserve(a, ws);
         if (ws.end - ws.base < FMGI_RING_CODES) return; /* overflow (counted in reserve) */
-        uint32_t *hist = (uint32_t *)ring + FMGI_RING_CODES + 64;
+        uint32_t *hist = (uint32_t *)ring + FMGI_RING_HIST;
         const uint64_t live = __ballot(true);
         const uint32_t nl = (uint32_t)__popcll(live);
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
@@ -912,15 +919,17 @@ struct AccStream {
        Every wave keeps, per fold tile, one open FMGI_BUCKET_BLOCK-code block of the pool (its private
        bucket: no other wave writes it). A ring flush sorts the ring by tile and appends each tile's run to
        the wave's bucket of that tile; a bucket that fills is closed (its length recorded) and a fresh block
-       is taken with one atomic on the pool cursor, the block's tile recorded beside it. The fold lists the
-       blocks by tile and reads them as whole 4-KB runs. Per-wave state, in the wave's LDS info table:
-       info[t] = {open block (kNoBlock: none), codes in it, (flush temporaries)}. */
+       is taken with one atomic on the pool cursor, the block's tile recorded beside it. Runs are padded
+       with sentinels to a multiple of 4 codes, so every bucket fill is 16-B aligned and a flush is stored
+       as whole 16-B quads. The fold lists the blocks by tile and reads them as whole 4-KB runs. Per-wave
+       state, in the wave's LDS info table: info[t] = {open block (kNoBlock: none), codes in it, (flush
+       temporaries)}. */
     static constexpr uint32_t kNoBlock = 0xFFFFFFFFu;
+    static constexpr uint32_t kSent = 0xFFFFFFFFu;
     static constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
+    static_assert(FMGI_RING_PAD >= 3 * FMGI_PRESORT_MAX_TILES, "a padded flush must fit the ring");
 
-    static __device__ __forceinline__ uint4 *bucket_info(uint32_t *ring) {
-        return (uint4 *)(ring + FMGI_RING_CODES + 128);
-    }
+    static __device__ __forceinline__ uint4 *bucket_info(uint32_t *ring) { return (uint4 *)(ring + FMGI_RING_INFO); }
     /* at the start of the bake: no wave has an open bucket */
     static __device__ __forceinline__ void bucket_init(const BakeArgs &a, uint32_t *ring) {
         uint4 *info = bucket_info(ring);
@@ -938,6 +947,7 @@ struct AccStream {
     /* the fallback of an exhausted pool: the code's colour, added to the int64 lightmap with device
        atomics (exact, order-free, as AccFx3) */
     static __device__ __forceinline__ void bucket_atomic(const BakeArgs &a, uint32_t code) {
+        if (code == kSent) return;
         const uint4 cc = a.colpack[code & 1023];
         unsigned long long *q = a.lm + 4 * (size_t)(code >> 10);
         const unsigned long long r = cc.x;
@@ -946,46 +956,61 @@ struct AccStream {
         atomicAdd(q + 2, r + (unsigned long long)(long long)(int32_t)cc.z);
     }
 
-    /* place tile t's run of cnt codes (ring run start `start`) in the wave's bucket: info[t] becomes
-       {first block, offset in it, run start, second block} (the second only when the bucket fills up) */
+    /* place tile t's padded run of pc codes (pc % 4 == 0; ring run start `start`) in the wave's bucket:
+       info[t] becomes {first block, offset in it, run start, second block} (the second only when the
+       bucket fills up) */
     static __device__ __forceinline__ void bucket_place(const BakeArgs &a, uint4 *info, int t, uint32_t start,
-                                                        uint32_t cnt) {
+                                                        uint32_t pc) {
         const uint4 st = info[t];
-        const uint32_t room = BP - st.y; /* 0 without an open bucket (y = BP) */
+        const uint32_t room = BP - st.y; /* 0 without an open bucket (y = BP); a multiple of 4 */
         uint32_t second = kNoBlock;
-        if (cnt <= room) {
-            if (cnt == room && st.x != kNoBlock) a.block_len[st.x] = BP;
+        if (pc <= room) {
+            if (pc == room && st.x != kNoBlock) a.block_len[st.x] = BP;
         } else {
             if (room && st.x != kNoBlock) a.block_len[st.x] = BP;
             second = bucket_alloc(a, (uint32_t)t);
-            if (cnt - room == BP && second != kNoBlock) a.block_len[second] = BP;
+            if (pc - room == BP && second != kNoBlock) a.block_len[second] = BP;
         }
         info[t] = make_uint4(st.x, st.y, start, second);
     }
-    /* the code of rank rk in tile t's run goes to ... (info as bucket_place left it) */
-    static __device__ __forceinline__ void bucket_store(const BakeArgs &a, uint4 inf, uint32_t rk, uint32_t code) {
+    /* the code of rank rk (a quad: rk % 4 == 0) in tile t's run goes to ... (info as bucket_place left it) */
+    static __device__ __forceinline__ uint32_t *bucket_slot(const BakeArgs &a, uint4 inf, uint32_t rk) {
         const uint32_t room = BP - inf.y;
         const bool first = rk < room;
         const uint32_t blk = first ? inf.x : inf.w;
-        if (blk == kNoBlock) bucket_atomic(a, code);
-        else a.stream[(uint64_t)blk * BP + (first ? inf.y + rk : rk - room)] = code;
+        return blk == kNoBlock ? nullptr : a.stream + ((uint64_t)blk * BP + (first ? inf.y + rk : rk - room));
+    }
+    static __device__ __forceinline__ void bucket_store(const BakeArgs &a, uint4 inf, uint32_t rk, uint32_t code) {
+        uint32_t *d = bucket_slot(a, inf, rk);
+        if (d) *d = code;
+        else bucket_atomic(a, code);
+    }
+    static __device__ __forceinline__ void bucket_store4(const BakeArgs &a, uint4 inf, uint32_t rk, uint4 q) {
+        uint4 *d = (uint4 *)bucket_slot(a, inf, rk);
+        if (d) {
+            *d = q;
+        } else {
+            bucket_atomic(a, q.x), bucket_atomic(a, q.y), bucket_atomic(a, q.z), bucket_atomic(a, q.w);
+        }
     }
     /* ... and the bucket after the run: the first block while the run fit in it, else the second */
-    static __device__ __forceinline__ void bucket_advance(uint4 *info, int t, uint32_t cnt) {
+    static __device__ __forceinline__ void bucket_advance(uint4 *info, int t, uint32_t pc) {
         const uint4 inf = info[t];
         const uint32_t room = BP - inf.y;
-        info[t] = cnt <= room ? make_uint4(inf.x, inf.y + cnt, 0u, kNoBlock) : make_uint4(inf.w, cnt - room, 0u, kNoBlock);
+        info[t] = pc <= room ? make_uint4(inf.x, inf.y + pc, 0u, kNoBlock) : make_uint4(inf.w, pc - room, 0u, kNoBlock);
     }
 
     /* bucketed stream: append ring[0, n) to the wave's tile buckets. With every lane live (the common
-       case), each lane holds 16 codes while an LDS histogram counts them per tile, a scan gives each tile's
-       run start, and the codes are scattered back into the ring sorted by tile; the lane of tile t places
-       the run in its bucket (bucket_place), and the lanes store the sorted ring, consecutive lanes to
-       consecutive positions of one run. With lanes already done (the bake's tail) the ring is not sorted:
-       each code takes its rank in its run from a second pass over the histogram. Called where every live
-       lane of the wave is active. */
+       case), each lane holds 16 codes while an LDS histogram counts them per tile, a scan of the padded
+       counts gives each tile's run start, the codes are scattered back into the ring sorted by tile (the
+       pads filled with sentinels; the ring's overflow, which the padded runs may cover, is kept in a
+       register meanwhile), the lane of tile t places the run in its bucket (bucket_place), and the lanes
+       store the sorted ring as 16-B quads, consecutive lanes to consecutive quads of one run. With lanes
+       already done (the bake's tail) the ring is not sorted: each code takes its rank in its run from a
+       second pass over the histogram and is stored alone. Called where every live lane of the wave is
+       active. */
     static __device__ __forceinline__ void bucket_out(const BakeArgs &a, uint32_t *ring, uint32_t n) {
-        uint32_t *hist = ring + FMGI_RING_CODES + 64;
+        uint32_t *hist = ring + FMGI_RING_HIST;
         uint4 *info = bucket_info(ring);
         const uint64_t live = __ballot(true);
         const uint32_t nl = (uint32_t)__popcll(live);
@@ -1006,20 +1031,22 @@ struct AccStream {
                 }
             } else {
 #pragma unroll
-                for (int e = 0; e < 16; e++) cr[e] = 16 * r + e < n ? ring[16 * r + e] : 0xFFFFFFFFu;
+                for (int e = 0; e < 16; e++) cr[e] = 16 * r + e < n ? ring[16 * r + e] : kSent;
             }
+            const uint32_t ov = ring[FMGI_RING_CODES + r]; /* the overflow (append moves it after the flush) */
 #pragma unroll
             for (int e = 0; e < 16; e++)
-                if (cr[e] != 0xFFFFFFFFu) atomicAdd(&hist[cr[e] >> shift], 1u);
+                if (cr[e] != kSent) atomicAdd(&hist[cr[e] >> shift], 1u);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
             const uint32_t cnt = (int)r < P ? hist[r] : 0u; /* lane t: tile t */
-            uint32_t incl = cnt;
+            const uint32_t pc = (cnt + 3u) & ~3u;
+            uint32_t incl = pc;
             for (int off = 1; off < 64; off <<= 1) {
                 const uint32_t o = __shfl_up(incl, off, 64);
                 if ((int)r >= off) incl += o;
             }
-            const uint32_t start = incl - cnt;
+            const uint32_t start = incl - pc, quads = __shfl(incl, 63, 64) >> 2;
             if ((int)r < P) hist[r] = start;
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1028,31 +1055,32 @@ struct AccStream {
                 uint32_t o[8];
 #pragma unroll
                 for (int e = 0; e < 8; e++)
-                    o[e] = cr[h + e] != 0xFFFFFFFFu ? atomicAdd(&hist[cr[h + e] >> shift], 1u) : 0u;
+                    o[e] = cr[h + e] != kSent ? atomicAdd(&hist[cr[h + e] >> shift], 1u) : 0u;
 #pragma unroll
                 for (int e = 0; e < 8; e++)
-                    if (cr[h + e] != 0xFFFFFFFFu) ring[o[e]] = cr[h + e];
+                    if (cr[h + e] != kSent) ring[o[e]] = cr[h + e];
             }
-            if ((int)r < P && cnt) bucket_place(a, info, (int)r, start, cnt);
+            for (uint32_t k = cnt; k < pc; k++) ring[start + k] = kSent;
+            if (cnt) bucket_place(a, info, (int)r, start, pc);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-#pragma unroll 4
-            for (uint32_t i = r; i < n; i += 64) {
-                const uint32_t code = ring[i];
-                const uint4 inf = info[code >> shift];
-                bucket_store(a, inf, i - inf.z, code);
+            for (uint32_t q = r; q < quads; q += 64) {
+                const uint4 v = ((const uint4 *)ring)[q];
+                const uint4 inf = info[v.x >> shift]; /* a run starts with a code: v.x is one */
+                bucket_store4(a, inf, 4 * q - inf.z, v);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            if ((int)r < P && cnt) bucket_advance(info, (int)r, cnt);
+            if (cnt) bucket_advance(info, (int)r, pc);
+            ring[FMGI_RING_CODES + r] = ov;
         } else {
             for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
             for (int t = (int)r; t < P; t += (int)nl) {
-                const uint32_t cnt = hist[t];
-                if (cnt) bucket_place(a, info, t, 0u, cnt);
-                hist[t + 64 * 0] = cnt;
+                const uint32_t cnt = hist[t], pc = (cnt + 3u) & ~3u;
+                if (cnt) bucket_place(a, info, t, 0u, pc);
+                for (uint32_t k = cnt; k < pc; k++) bucket_store(a, info[t], k, kSent);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1069,7 +1097,7 @@ struct AccStream {
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
             for (int t = (int)r; t < P; t += (int)nl)
-                if (hist[t]) bucket_advance(info, t, hist[t]);
+                if (hist[t]) bucket_advance(info, t, (hist[t] + 3u) & ~3u);
         }
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1200,7 +1228,7 @@ __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
  */
 #ifdef FMGI_WAVES_PER_EU /* experiment builds: ask the register allocator for this occupancy */
 #define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(FMGI_WAVES_PER_EU)))
-#else /* ScanGrid: 5 waves/SIMD (96 VGPRs, no spills; unconstrained it takes 98 and 4 waves, -2.5 %) */
+#else /* ScanGrid: 4 waves/SIMD (108 VGPRs, no spills): with the walls staged, LDS holds a CU to 16 waves anyway */
 #define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(Scan::kMinWaves)))
 #endif
 template <class Scan, class Acc, bool TRACE>
@@ -1572,6 +1600,13 @@ const void *kernel_ptr(bool trace) {
 }
 
 const void *bake_kernel(int kernel, int accum, bool trace) {
+    if (kernel == (2 | FMGI_KVAR_AXES)) {
+        if (accum == 2) return kernel_ptr<ScanGridAxes, AccState>(trace);
+        if (accum == 3) return kernel_ptr<ScanGridAxes, AccNone>(trace);
+        if (accum == 4) return kernel_ptr<ScanGridAxes, AccStream>(trace);
+        return kernel_ptr<ScanGridAxes, AccFx3>(trace);
+    }
+    kernel &= ~FMGI_KVAR_AXES;
     if (kernel == 2) {
         if (accum == 2) return kernel_ptr<ScanGrid, AccState>(trace);
         if (accum == 3) return kernel_ptr<ScanGrid, AccNone>(trace);
@@ -1650,7 +1685,12 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         else if (accum == 3) launch3<ScanHybrid, AccNone>(a, trace, grid, blk, lds, s);
         else if (accum == 4) launch3<ScanHybrid, AccStream>(a, trace, grid, blk, lds, s);
         else launch3<ScanHybrid, AccFx3>(a, trace, grid, blk, lds, s);
-    } else if (kernel == 2) { /* FMGI_KERNEL_GRID */
+    } else if (kernel == (2 | FMGI_KVAR_AXES)) { /* FMGI_KERNEL_GRID, closed box */
+        if (accum == 2) launch3<ScanGridAxes, AccState>(a, trace, grid, blk, lds, s);
+        else if (accum == 3) launch3<ScanGridAxes, AccNone>(a, trace, grid, blk, lds, s);
+        else if (accum == 4) launch3<ScanGridAxes, AccStream>(a, trace, grid, blk, lds, s);
+        else launch3<ScanGridAxes, AccFx3>(a, trace, grid, blk, lds, s);
+    } else if ((kernel & ~FMGI_KVAR_AXES) == 2) { /* FMGI_KERNEL_GRID */
         if (accum == 2) launch3<ScanGrid, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanGrid, AccNone>(a, trace, grid, blk, lds, s);
         else if (accum == 4) launch3<ScanGrid, AccStream>(a, trace, grid, blk, lds, s);

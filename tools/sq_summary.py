@@ -1,12 +1,16 @@
 #!/usr/bin/env python
-"""Summarise a gpu_session.sh `sq` step (two rocprofv3 --pmc passes of SQ counters) into per-dispatch
-instruction counts of the bake kernel, recorded in profiles/sq_issue.json under the bench config name
-(bench.py reads SQ_INSTS_VALU per launch for its issue roofline).
+"""Summarise the counter passes of one gpu_session.sh session (steps sq, sq3, grbm, tcp, clock) into
+per-dispatch counters of the bake kernel, recorded in profiles/sq_issue.json under the bench config name.
+bench.py derives its `roofline.issue` block from this file (clock, SIMD cycles, wave-cycle split,
+vector-memory path busy fractions).
 
-  python tools/sq_summary.py gpurun_out/s47 box200 [--out profiles/sq_issue.json]
+  python tools/sq_summary.py profiles/r03/final box200 [--out profiles/sq_issue.json]
 
-The SQ_*_CYCLES / SQ_ACTIVE_* / SQ_WAIT_* counters are in units of 4 cycles on gfx9 (quad-cycles);
-they are kept as reported. SQ_INSTS_* are wave-instruction counts."""
+<session>/<pass>/**/*counter_collection.csv are rocprofv3 --pmc outputs (one pass per directory);
+<session>/bench_clock.json, if present, is the FMGI_CLOCK_STAMP build's bench line (in-kernel
+s_memtime / s_memrealtime clock). SQ_*_CYCLES / SQ_ACTIVE_* / SQ_WAIT_* are kept as reported (units of 4
+cycles on gfx9; only their ratios are used); SQ_INSTS_* are wave-instruction counts; GRBM_GUI_ACTIVE is
+summed over the 8 XCDs; TA_/TD_/TCP_ *_sum are summed over the 256 CUs."""
 import argparse
 import collections
 import csv
@@ -14,37 +18,55 @@ import glob
 import json
 import os
 
+PASSES = ("sq1", "sq2", "sq3", "grbm", "tcp")
+
 
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("session")
     ap.add_argument("config")
+    ap.add_argument("--kernel", default="k_bake")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "sq_issue.json"))
     a = ap.parse_args()
     tot = collections.defaultdict(float)
     ids = collections.defaultdict(set)
+    src = {}
     kernel = None
-    for step in ("sq1", "sq2"):
+    for step in PASSES:
         for p in glob.glob(os.path.join(a.session, step, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(p)):
-                if "k_bake" not in r["Kernel_Name"]:
+                if a.kernel not in r["Kernel_Name"]:
                     continue
                 kernel = r["Kernel_Name"]
-                tot[r["Counter_Name"]] += float(r["Counter_Value"])
-                ids[r["Counter_Name"]].add(r["Dispatch_Id"])
+                c = r["Counter_Name"]
+                if c in src and src[c] != step:
+                    continue  # a counter collected in several passes: keep the first pass's value
+                src[c] = step
+                tot[c] += float(r["Counter_Value"])
+                ids[c].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
     if not tot:
-        raise SystemExit("no k_bake dispatch in the SQ files")
+        raise SystemExit(f"no {a.kernel} dispatch in the counter files of {a.session}")
     per = {k: tot[k] / max(len(ids[k]), 1) for k in sorted(tot)}
-    data = json.load(open(a.out)) if os.path.exists(a.out) else {}
-    data[a.config] = {
+    rec = {
         "kernel": kernel,
-        "source": f"{a.session}: rocprofv3 --pmc SQ counters in two passes (tools/gpu_session.sh step sq), per dispatch",
+        "source": f"{a.session}/{{{','.join(PASSES)}}}: rocprofv3 --pmc passes (tools/gpu_session.sh steps sq, sq3, "
+                  "grbm, tcp), per dispatch",
+        "pass_of": src,
         "per_launch": per,
     }
+    clk = os.path.join(a.session, "bench_clock.json")
+    if os.path.exists(clk):
+        d = json.load(open(clk))
+        rec["clock_ghz"] = d["in_kernel_clock_ghz"]
+        rec["clock_source"] = f"{clk}: FMGI_CLOCK_STAMP build, s_memtime / s_memrealtime (100 MHz) per wave"
+    if per.get("GRBM_GUI_ACTIVE"):
+        rec["grbm_cycles_per_xcd"] = per["GRBM_GUI_ACTIVE"] / 8.0
+    data = json.load(open(a.out)) if os.path.exists(a.out) else {}
+    data[a.config] = rec
     with open(a.out, "w") as fh:
-        json.dump(data, fh, indent=1)
+        json.dump(data, fh, indent=1, sort_keys=True)
     for k, v in per.items():
-        print(f"{k:28s} {v:.4e}")
+        print(f"{k:40s} {v:.4e}  ({src[k]})")
 
 
 if __name__ == "__main__":

@@ -1,5 +1,6 @@
 // tools/valu_peak.hip -- measured instruction-issue ceilings of one MI355X: wave64 VALU instructions per
-// second for dependency-free v_fma_f32 and v_fma_f64 streams at 1, 2, 4, 5 and 8 waves per SIMD, on
+// second for dependency-free v_fma_f32 streams (three VGPR sources, as compiled code reads them, and one
+// VGPR source with inline constants: no operand-bank conflicts) and v_fma_f64, at 1-8 waves per SIMD, on
 // launches of >= 50 ms (the chip's clock under sustained load, not a 0.3-ms burst), with the in-kernel
 // clock of every case measured per MI355X_MICROARCH.md "DVFS give-back" item 6: delta s_memtime / delta
 // s_memrealtime x 100 MHz, stamped by each wave around its loop (median over waves). Each lane runs 8
@@ -26,6 +27,11 @@ __global__ __launch_bounds__(256) void k_issue(float *out, unsigned long long *s
                          " v_fma_f32 %6, %6, %8, %9\n v_fma_f32 %7, %7, %8, %9"
                          : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7)
                          : "v"(m), "v"(c));
+        } else if (MODE == 2) { // 8 x v_fma_f32 with one VGPR source (inline constants: no operand-bank conflicts)
+            asm volatile("v_fma_f32 %0, %0, 0.5, 1.0\n v_fma_f32 %1, %1, 0.5, 1.0\n v_fma_f32 %2, %2, 0.5, 1.0\n"
+                         " v_fma_f32 %3, %3, 0.5, 1.0\n v_fma_f32 %4, %4, 0.5, 1.0\n v_fma_f32 %5, %5, 0.5, 1.0\n"
+                         " v_fma_f32 %6, %6, 0.5, 1.0\n v_fma_f32 %7, %7, 0.5, 1.0"
+                         : "+v"(a0), "+v"(a1), "+v"(a2), "+v"(a3), "+v"(a4), "+v"(a5), "+v"(a6), "+v"(a7));
         } else { // 8 x v_fma_f64
             asm volatile("v_fma_f64 %0, %0, %8, %9\n v_fma_f64 %1, %1, %8, %9\n v_fma_f64 %2, %2, %8, %9\n"
                          " v_fma_f64 %3, %3, %8, %9\n v_fma_f64 %4, %4, %8, %9\n v_fma_f64 %5, %5, %8, %9\n"
@@ -97,6 +103,7 @@ int main() {
     hipMalloc(&d_out, (size_t)cus * 8 * 256 * sizeof(float));
     hipMalloc(&d_st, (size_t)cus * 8 * 4 * 2 * sizeof(unsigned long long));
     for (int w : {1, 2, 4, 5, 8}) run<0>("v_fma_f32", cus, w, d_out, d_st);
+    for (int w : {1, 2, 4, 5, 8}) run<2>("v_fma_f32_1vgpr", cus, w, d_out, d_st);
     for (int w : {1, 5, 8}) run<1>("v_fma_f64", cus, w, d_out, d_st);
     printf("{\"cus\": %d, \"clock_khz\": %d}\n", cus, p.clockRate);
     return 0;
