@@ -379,6 +379,143 @@ GridBuild build_grid(const FilterBuild &fb) {
     return gb;
 }
 
+/*
+ * Floor plan of the walls for ScanHybrid's wall pass (fmgi_kernels.hip plan_walls). The x- and y-axis
+ * records of the filter image are vertical walls: seen from above, a segment x = X, y in
+ * [cu - hwu, cu + hwu] (or y = Y, x in [...]). A uniform nx x ny grid of square cells covers the walls and
+ * the sources; each cell lists (as u16 indices r of 32-B records in the filter image: byte offset 32 r) every
+ * wall whose footprint, grown by `slack`, overlaps it. A lane walks the cells its ray crosses, nearest
+ * first, tests the listed walls it faces with the filter's own float ops, and stops once the ray leaves
+ * the cell past the 2^-11 band above its best key. Why that finds every wall the filter would find with a
+ * key inside the band: a wall that passes its filter test at key f contains the computed hit point, which
+ * lies within |d| f 2^-20 + a few ulps of the exact ray point at parameter f; that ray point lies in a cell
+ * the walk visits (f <= band < the exit parameter of the last cell, up to the same rounding), and the wall
+ * is registered in every cell within `slack` of its footprint, which bounds both roundings and the walk's
+ * own cell arithmetic. Walls beyond the band cannot win or change the separation test (grid_phase1_sorted).
+ * Layout (LDS, after the plane image): {x0, y0, ics, cs} {nx | ny << 16, ncells, nentries, 0}, then
+ * u16 start[ncells + 1] (cell i's entries are entry[start[i] .. start[i + 1])), then u16 entry[].
+ */
+struct PlanBuild {
+    float x0 = 0, y0 = 0, ics = 0, cs = 0;
+    int nx = 0, ny = 0;
+    std::vector<uint16_t> start, entry;
+    bool ok = false;
+    std::vector<char> blob() const {
+        std::vector<char> b(32 + 2 * (start.size() + entry.size()));
+        const float h0[4] = {x0, y0, ics, cs};
+        const int32_t h1[4] = {nx | (ny << 16), (int32_t)start.size() - 1, (int32_t)entry.size(), 0};
+        memcpy(b.data(), h0, 16);
+        memcpy(b.data() + 16, h1, 16);
+        memcpy(b.data() + 32, start.data(), 2 * start.size());
+        memcpy(b.data() + 32 + 2 * start.size(), entry.data(), 2 * entry.size());
+        b.resize((b.size() + 15) & ~(size_t)15);
+        return b;
+    }
+};
+
+PlanBuild build_plan(const FilterBuild &fb, const fmgi_rect *srcs, int ns) {
+    PlanBuild pb;
+    struct Seg { double a_lo, a_hi, b_lo, b_hi; int r; }; /* footprint box in (x, y) and record index */
+    std::vector<Seg> segs;
+    for (int a = 0; a < 2; a++)
+        for (int j = 0; j < fb.J[a]; j++)
+            for (int c = 0; c < 2; c++) {
+                if (j >= (int)fb.cls[a][c].size()) continue;
+                const FilterRec &f = fb.cls[a][c][j];
+                const int r = 2 * ((a == 0 ? 0 : fb.J[0]) + j) + c;
+                const double lo_u = (double)f.cu - f.hwu, hi_u = (double)f.cu + f.hwu;
+                /* x-walls (a = 0): x = plane, y = u; y-walls: y = plane, x = u */
+                if (a == 0) segs.push_back({f.plane, f.plane, lo_u, hi_u, r});
+                else segs.push_back({lo_u, hi_u, f.plane, f.plane, r});
+            }
+    if (segs.empty() || fb.J[0] + fb.J[1] > 16000) return pb; /* u16 record indices */
+    double xlo = 1e300, xhi = -1e300, ylo = 1e300, yhi = -1e300;
+    for (const Seg &s : segs) {
+        xlo = std::min(xlo, s.a_lo), xhi = std::max(xhi, s.a_hi);
+        ylo = std::min(ylo, s.b_lo), yhi = std::max(yhi, s.b_hi);
+    }
+    for (int i = 0; i < ns; i++)
+        for (int k = 0; k < 4; k++) {
+            const double x = (double)srcs[i].pos.s[0] + ((k & 1) ? srcs[i].width.s[0] : 0.f) + ((k & 2) ? srcs[i].height.s[0] : 0.f);
+            const double y = (double)srcs[i].pos.s[1] + ((k & 1) ? srcs[i].width.s[1] : 0.f) + ((k & 2) ? srcs[i].height.s[1] : 0.f);
+            xlo = std::min(xlo, x), xhi = std::max(xhi, x), ylo = std::min(ylo, y), yhi = std::max(yhi, y);
+        }
+    const double ex = std::max(xhi - xlo, 1e-6), ey = std::max(yhi - ylo, 1e-6);
+    /* the cell size: minimise the expected cost of one walk, (cells visited) x (1 + entries per cell:
+       the faced half, doubled for rays that start beside walls), with 1 + 1.27 l / cs cells visited for a horizontal run l of 0.6 x the walls' median height
+       (a ray between floor and ceiling; fitted on example.png and the 30-room layout, tests/test_plan.py),
+       over cells from 1/4 to 1/64 of the larger extent (FMGI_PLAN_CELLS forces the cells along the larger
+       extent, experiments) */
+    double run = 1.0;
+    {
+        std::vector<double> hs;
+        for (int a = 0; a < 2; a++)
+            for (int c = 0; c < 2; c++)
+                for (const FilterRec &f : fb.cls[a][c]) hs.push_back(2.0 * ((double)f.hwv - fb.margin));
+        if (!hs.empty()) {
+            std::nth_element(hs.begin(), hs.begin() + hs.size() / 2, hs.end());
+            run = std::max(0.6 * hs[hs.size() / 2], 1e-3);
+        }
+    }
+    auto regs = [&](double cs, double x0, double y0, double sl, int nx, int ny, std::vector<uint16_t> *st,
+                    std::vector<uint16_t> *en) -> size_t {
+        std::vector<std::vector<uint16_t>> cell(st ? (size_t)nx * ny : 0);
+        size_t n = 0;
+        for (const Seg &s : segs) {
+            const int i0 = std::max(0, (int)std::floor((s.a_lo - sl - x0) / cs));
+            const int i1 = std::min(nx - 1, (int)std::floor((s.a_hi + sl - x0) / cs));
+            const int j0 = std::max(0, (int)std::floor((s.b_lo - sl - y0) / cs));
+            const int j1 = std::min(ny - 1, (int)std::floor((s.b_hi + sl - y0) / cs));
+            for (int jy = j0; jy <= j1; jy++)
+                for (int ix = i0; ix <= i1; ix++) {
+                    n++;
+                    if (st) cell[(size_t)jy * nx + ix].push_back((uint16_t)s.r);
+                }
+        }
+        if (st) {
+            st->assign(1, 0);
+            en->clear();
+            for (const auto &v : cell) {
+                en->insert(en->end(), v.begin(), v.end());
+                st->push_back((uint16_t)std::min<size_t>(en->size(), 65535));
+            }
+        }
+        return n;
+    };
+    const double big = std::max(ex, ey);
+    int m_lo = 4, m_hi = 64;
+    if (const char *pe = getenv("FMGI_PLAN_CELLS"))
+        if (atoi(pe) >= 1 && atoi(pe) <= 256) m_lo = m_hi = atoi(pe);
+    double best = 1e300;
+    for (int m = m_lo; m <= m_hi; m++) {
+        const double cs = big / m;
+        /* slack: the filter margin (the footprint's own growth already holds it along the wall; across
+           the wall it is needed here), plus 1/64 cell for the walk's float cell arithmetic */
+        const double sl = (double)fb.margin + cs / 64 + fb.scale * 0x1p-18;
+        const double x0 = xlo - cs, y0 = ylo - cs;
+        const int nx = (int)std::ceil(ex / cs) + 3, ny = (int)std::ceil(ey / cs) + 3;
+        if ((int64_t)nx * ny > 4096 || nx > 255 || ny > 255) continue;
+        const size_t n = regs(cs, x0, y0, sl, nx, ny, nullptr, nullptr);
+        if (n > 60000) continue;
+        const double cost = (1.0 + 1.27 * run / cs) * (1.0 + (double)n / ((double)nx * ny));
+        if (cost < best) {
+            best = cost;
+            pb.cs = (float)cs;
+            pb.nx = nx;
+            pb.ny = ny;
+        }
+    }
+    if (best == 1e300) return pb;
+    const double cs = pb.cs; /* the float cell size the kernel uses */
+    pb.ics = (float)(1.0 / cs);
+    pb.x0 = (float)(xlo - cs);
+    pb.y0 = (float)(ylo - cs);
+    const double sl = (double)fb.margin + cs / 64 + fb.scale * 0x1p-18;
+    regs(cs, pb.x0, pb.y0, sl, pb.nx, pb.ny, &pb.start, &pb.entry);
+    pb.ok = pb.entry.size() < 65535;
+    return pb;
+}
+
 /* Exact deposit colour of every colour state (kernel: k_bake's `sid`), in fixed point. The float ops
    replay photonmap.cl:167-169,241-249 in the kernel's order, so the values are bit-identical. */
 std::vector<long long> colour_table() {
@@ -441,6 +578,8 @@ struct fmgi_context {
     int32_t *d_gidx = nullptr;
     int grid_cells = 0, grid_entries = 0;
     GridBuild h_grid; /* host copy (fmgi_grid_copy) */
+    PlanBuild h_plan; /* ScanHybrid's floor plan of the walls (fmgi_plan_copy); h_plan.ok: built */
+    int plan_off = -1; /* its byte offset in the hybrid image */
     int auto_kernel = FMGI_KERNEL_FAST;
     /* optional device timing (fmgi_set_timing) */
     bool timing = false;
@@ -814,9 +953,12 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->grid_cells = (int)gb.cells.size();
     c->grid_entries = (int)gb.idx.size();
     c->h_grid = gb;
-    /* ScanHybrid's image is the filter image followed by the plane image: its size must be this scene's
-       before the AUTO choice below asks which images fit LDS (also in host-only contexts) */
-    c->himg_bytes = c->fimg_bytes + c->gimg_bytes;
+    /* ScanHybrid's image is the filter image followed by the plane image and the floor plan: its size must
+       be this scene's before the AUTO choice below asks which images fit LDS (also in host-only contexts) */
+    c->h_plan = build_plan(fb, c->h_srcs.data(), (int)c->h_srcs.size());
+    const std::vector<char> plan_blob = c->h_plan.ok ? c->h_plan.blob() : std::vector<char>();
+    c->plan_off = c->h_plan.ok ? c->fimg_bytes + c->gimg_bytes : -1;
+    c->himg_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
     {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
@@ -876,10 +1018,11 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->d_gidx = nullptr;
     HIPCHK(upload(&c->d_gimg, gb.img));
     HIPCHK(upload(&c->d_gcells, gb.cells));
-    {   /* ScanHybrid's image: the filter image (a multiple of 64 B), then the plane image */
-        std::vector<char> both((size_t)c->fimg_bytes + (size_t)c->gimg_bytes);
+    {   /* ScanHybrid's image: the filter image (a multiple of 64 B), then the plane image, then the plan */
+        std::vector<char> both((size_t)c->himg_bytes);
         memcpy(both.data(), fb.img.data(), (size_t)c->fimg_bytes);
         memcpy(both.data() + c->fimg_bytes, gb.img.data(), (size_t)c->gimg_bytes);
+        if (!plan_blob.empty()) memcpy(both.data() + c->plan_off, plan_blob.data(), plan_blob.size());
         hipFree(c->d_himg);
         c->d_himg = nullptr;
         HIPCHK(upload(&c->d_himg, both));
@@ -1032,6 +1175,7 @@ static bool grid_axes_scene(const fmgi_context *c) {
     return c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES");
 }
 static int kernel_instance(const fmgi_context *c, int kernel) {
+    if (kernel == FMGI_KERNEL_HYBRID && c->plan_off >= 0 && !getenv("FMGI_NO_PLAN")) return kernel | FMGI_KVAR_PLAN;
     return kernel == FMGI_KERNEL_GRID && grid_axes_scene(c) ? (kernel | FMGI_KVAR_AXES) : kernel;
 }
 
@@ -1201,6 +1345,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
         a.grid_code_or = 0x40000000;
+        a.plan_off = c->plan_off;
     } else {
         a.fimg = c->d_fimg;
         a.fimg_bytes = c->fimg_bytes;
@@ -1545,6 +1690,15 @@ FMGI_API int fmgi_grid_sizes(const fmgi_context *c, int32_t sizes[5]) {
     for (int a = 0; a < 3; a++) sizes[a] = c->h_grid.J[a];
     sizes[3] = (int32_t)c->h_grid.cells.size();
     sizes[4] = (int32_t)c->h_grid.idx.size();
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_plan_copy(const fmgi_context *c, void *blob, int32_t *bytes) {
+    if (!c || !bytes) return set_err(FMGI_ERR_ARG, "fmgi_plan_copy: bad arguments");
+    const std::vector<char> b = c->h_plan.ok ? c->h_plan.blob() : std::vector<char>();
+    if (blob && *bytes < (int32_t)b.size()) return set_err(FMGI_ERR_ARG, "fmgi_plan_copy: buffer too small");
+    if (blob && !b.empty()) memcpy(blob, b.data(), b.size());
+    *bytes = (int32_t)b.size();
     return FMGI_OK;
 }
 

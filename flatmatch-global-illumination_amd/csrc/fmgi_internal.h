@@ -82,6 +82,7 @@ struct BakeArgs {
     int rects_off, srcs_off;
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
+    int plan_off;         /* ScanHybridPlan: byte offset of the floor plan in the image (-1: none)      */
     const uint32_t *fetch_tab;    /* fetch_nseg > 0: [f_begin, item_begin] pairs, f_begin ascending from 0:
                                      fetch f maps into the segment holding it (sums are order-free) */
     int fetch_nseg;
@@ -166,6 +167,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
 /* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
    FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */
 #define FMGI_KVAR_AXES 0x100
+#define FMGI_KVAR_PLAN 0x200 /* FMGI_KERNEL_HYBRID | this: the walls over the floor plan (BakeArgs::plan_off) */
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);

@@ -704,6 +704,65 @@ using ScanGrid = ScanGridT<false>;
 using ScanGridAxes = ScanGridT<true>;
 
 /*
+ * ScanHybrid's wall pass over the floor plan (Plan = true; tables: fmgi_api.cpp build_plan, which holds
+ * the argument why it finds every wall the filter pass would find inside the 2^-11 band). The lane walks
+ * the cells its ray crosses seen from above, nearest first, and tests the listed walls of the classes it
+ * faces with filter_axis's own float ops, so every key is the filter's bit for bit. A wall listed in
+ * several cells of the walk is tested once per cell: its repeat key equals the current winner's only
+ * when it is the winner itself (code == code1), and is then dropped, since it would pose as a tie;
+ * against L2 or beyond, fmed3 leaves L2 unchanged. The walk stops when the ray leaves a cell past the
+ * band above L1, or leaves the grid.
+ */
+__device__ __forceinline__ void plan_walls(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1, float &L2,
+                                           int &code1, unsigned &ntest) {
+    const char *pl = img + a.plan_off;
+    const float4 h0 = *(const float4 *)__builtin_assume_aligned(pl, 16); /* x0, y0, 1 / cs, cs */
+    const int4 h1 = *(const int4 *)__builtin_assume_aligned(pl + 16, 16);
+    const int nx = h1.x & 0xFFFF, ny = h1.x >> 16;
+    const uint16_t *st = (const uint16_t *)(pl + 32), *en = st + h1.y + 1;
+    const int r0y = 2 * a.fJ[0]; /* the first y-wall record */
+    const float rx = __builtin_amdgcn_rcpf(d.x), ry = __builtin_amdgcn_rcpf(d.y);
+    const int cx = d.x < 0.0f ? 0 : 1, cy = d.y < 0.0f ? 0 : 1; /* faced class per axis; next boundary side */
+    int ix = (int)fminf(fmaxf(floorf((s.x - h0.x) * h0.z), 0.0f), (float)(nx - 1));
+    int iy = (int)fminf(fmaxf(floorf((s.y - h0.y) * h0.z), 0.0f), (float)(ny - 1));
+    const int sx = d.x > 0.0f ? 1 : -1, sy = d.y > 0.0f ? 1 : -1;
+    for (int step = nx + ny; step > 0; step--) {
+        const int cell = iy * nx + ix;
+        const int e = st[cell + 1];
+        for (int k = st[cell]; k < e; k++) {
+            const int r = en[k];
+            const bool ay = r >= r0y;
+            if ((r & 1) != (ay ? cy : cx)) continue; /* a wall of the class the lane does not face */
+            const float *q = (const float *)(img + 32 * r);
+            const float4 q4 = *(const float4 *)__builtin_assume_aligned(q, 16); /* plane, cu, hwu, cv */
+            const float hwv = q[4];
+            const float f = (q4.x - (ay ? s.y : s.x)) * (ay ? ry : rx);
+            const float uu = fmaf(ay ? d.x : d.y, f, ay ? s.x : s.y) - q4.y;
+            const float vv = fmaf(d.z, f, s.z) - q4.w;
+            const int code = ((ay ? 1 : 0) << 16) | ((r >> 1) - (ay ? a.fJ[0] : 0));
+            const int ok = (int)(f >= 0.0f) & (int)(fabsf(uu) <= q4.z) & (int)(fabsf(vv) <= hwv) & (int)(code != code1);
+            const float key = ok ? f : INFINITY;
+            const bool lt = key < L1;
+            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+            code1 = lt ? code : code1;
+            L1 = lt ? key : L1;
+            ntest++;
+        }
+        const float tx = d.x == 0.0f ? INFINITY : (fmaf((float)(ix + cx), h0.w, h0.x) - s.x) * rx;
+        const float ty = d.y == 0.0f ? INFINITY : (fmaf((float)(iy + cy), h0.w, h0.y) - s.y) * ry;
+        const bool alongx = tx < ty;
+        if (!((alongx ? tx : ty) <= L1 * 1.00048828125f)) break; /* past the band (or NaN) */
+        if (alongx) {
+            ix += sx;
+            if ((unsigned)ix >= (unsigned)nx) break;
+        } else {
+            iy += sy;
+            if ((unsigned)iy >= (unsigned)ny) break;
+        }
+    }
+}
+
+/*
  * ScanHybrid: the reference's apartment layouts have few floor/ceiling planes holding many records
  * (one floor and one ceiling rect per room) and walls on many planes. Phase 1 takes the floor/ceiling
  * axis through ScanGrid's cells (one cell lookup instead of a filter pass over every room's floor) and
@@ -711,7 +770,8 @@ using ScanGridAxes = ScanGridT<true>;
  * candidate sets and the keys are theirs, so phase 2, the separation test and the fallback are
  * ScanFast's. Grid candidates carry the rect index with the 0x40000000 flag (BakeArgs::grid_code_or).
  */
-struct ScanHybrid {
+template <bool Plan>
+struct ScanHybridT {
     static constexpr bool kLds = true;
     static constexpr bool kCoop = false;
     static constexpr int kMinWaves = 1; /* k_bake occupancy floor for the register allocator */
@@ -721,8 +781,13 @@ struct ScanHybrid {
         int code1 = -1;
         unsigned ntest = 0;
         grid_axis<2>(a, lds + a.hyb_off, 128 * (a.gJ[0] + a.gJ[1]), a.gJ[2], src, dir, L1, L2, code1, ntest);
-        filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
-        filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
+        if (Plan) { /* the walls the ray's floor-plan cells list, nearest cells first, after the floors */
+            plan_walls(a, lds, src, dir, L1, L2, code1, ntest);
+        } else {
+            filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
+            filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
+            ntest += (unsigned)(a.fJ[0] + a.fJ[1]);
+        }
         cptr<int32_t> G = (cptr<int32_t>)a.general;
         for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
             const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
@@ -732,7 +797,7 @@ struct ScanHybrid {
             code1 = lt ? ((3 << 16) | g) : code1;
             L1 = lt ? key : L1;
         }
-        st.tests += ntest + (uint32_t)(a.fJ[0] + a.fJ[1] + a.ngeneral);
+        st.tests += ntest + (uint32_t)a.ngeneral;
         if (L1 == INFINITY) {
             h.best = INFINITY;
             h.idx = -1;
@@ -762,6 +827,9 @@ struct ScanHybrid {
         finish_hit(a, hit, best, src, dir, h);
     }
 };
+
+using ScanHybrid = ScanHybridT<false>;
+using ScanHybridPlan = ScanHybridT<true>;
 
 /* ---- accumulation policies -------------------------------------------------------------------- */
 
@@ -1606,7 +1674,13 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
         if (accum == 4) return kernel_ptr<ScanGridAxes, AccStream>(trace);
         return kernel_ptr<ScanGridAxes, AccFx3>(trace);
     }
-    kernel &= ~FMGI_KVAR_AXES;
+    if (kernel == (4 | FMGI_KVAR_PLAN)) {
+        if (accum == 2) return kernel_ptr<ScanHybridPlan, AccState>(trace);
+        if (accum == 3) return kernel_ptr<ScanHybridPlan, AccNone>(trace);
+        if (accum == 4) return kernel_ptr<ScanHybridPlan, AccStream>(trace);
+        return kernel_ptr<ScanHybridPlan, AccFx3>(trace);
+    }
+    kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN);
     if (kernel == 2) {
         if (accum == 2) return kernel_ptr<ScanGrid, AccState>(trace);
         if (accum == 3) return kernel_ptr<ScanGrid, AccNone>(trace);
@@ -1680,6 +1754,11 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
     if (kernel == FMGI_KERNEL_FAST_COOP) {
         if (accum != 4 || trace) return hipErrorInvalidValue; /* cooperative lanes: stream accumulation only */
         launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
+    } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */
+        if (accum == 2) launch3<ScanHybridPlan, AccState>(a, trace, grid, blk, lds, s);
+        else if (accum == 3) launch3<ScanHybridPlan, AccNone>(a, trace, grid, blk, lds, s);
+        else if (accum == 4) launch3<ScanHybridPlan, AccStream>(a, trace, grid, blk, lds, s);
+        else launch3<ScanHybridPlan, AccFx3>(a, trace, grid, blk, lds, s);
     } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
         if (accum == 2) launch3<ScanHybrid, AccState>(a, trace, grid, blk, lds, s);
         else if (accum == 3) launch3<ScanHybrid, AccNone>(a, trace, grid, blk, lds, s);

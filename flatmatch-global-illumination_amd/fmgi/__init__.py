@@ -206,6 +206,22 @@ class Context:
         return {"J": [int(x) for x in sz[:3]], "planes": planes[: 2 * npairs], "cells": cells, "recs": recs,
                 "idx": idx}
 
+    def plan_tables(self) -> dict | None:
+        """FMGI_KERNEL_HYBRID's floor plan of the walls (include/flatmatch_gi.h fmgi_plan_copy), or None."""
+        n = C.c_int32(0)
+        check(self.lib.fmgi_plan_copy(self.h, None, C.byref(n)), "fmgi_plan_copy")
+        if n.value == 0:
+            return None
+        blob = np.zeros(n.value, np.uint8)
+        check(self.lib.fmgi_plan_copy(self.h, _ptr(blob), C.byref(n)), "fmgi_plan_copy")
+        h0 = blob[:16].view(np.float32)
+        h1 = blob[16:32].view(np.int32)
+        ncells, nent = int(h1[1]), int(h1[2])
+        u16 = blob[32:].view(np.uint16)
+        return {"x0": h0[0], "y0": h0[1], "ics": h0[2], "cs": h0[3], "nx": int(h1[0]) & 0xFFFF,
+                "ny": int(h1[0]) >> 16, "start": u16[: ncells + 1].copy(),
+                "entry": u16[ncells + 1 : ncells + 1 + nent].copy()}
+
     def device_sincosf(self, x: np.ndarray, library: bool = False):
         """The samplers' sin/cos on the device (the restatement), or with library=True the device
         library's sinf/cosf that it restates."""

@@ -280,6 +280,13 @@ int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);
    append}, since the last fmgi_reset_stats; all zero in the normal library. */
 int fmgi_get_stage_cycles(fmgi_context *ctx, uint64_t out[16]);
 int fmgi_grid_copy(const fmgi_context *ctx, void *planes, void *cells, float *recs, int32_t *idx);
+/* FMGI_KERNEL_HYBRID's floor plan of the walls (built by fmgi_set_scene; host-only contexts too; the
+   hybrid scan walks it unless FMGI_NO_PLAN is set): *bytes = its size (0: no plan for this scene); with
+   blob != NULL and *bytes >= that size, copies it: {float x0, y0, 1 / cs, cs}, {int32 nx | ny << 16,
+   ncells, nentries, 0}, u16 start[ncells + 1], u16 entry[nentries] (cell (ix, iy) = iy * nx + ix lists
+   entry[start[i] .. start[i + 1]]: 32-B records of the filter image, record r at byte 32 r; x walls
+   first, r & 1 = the class, +n = 0). */
+int fmgi_plan_copy(const fmgi_context *ctx, void *blob, int32_t *bytes);
 
 /* Host helpers exported for tests (no device needed). */
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);

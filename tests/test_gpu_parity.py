@@ -117,6 +117,25 @@ def test_box_traces_without_axes_mode(torch_cuda, box200, offsets):
         os.environ.pop("FMGI_NO_AXES", None)
 
 
+def test_layout_traces_without_floor_plan(torch_cuda, example_scene, offsets):
+    """The hybrid scan walks the floor plan of the walls (plan_walls); FMGI_NO_PLAN=1 runs its filter pass
+    over every wall instead: both give the oracle's traces and lightmap."""
+    spa = 6_500_000
+    L = _oracle_plan(example_scene, spa, offsets)
+    ctx = _ctx(example_scene, spa, offsets)
+    olm, _ = O.bake(example_scene, L, 40_000, 52_000)
+    for env in ("0", "1"):
+        if env == "1":
+            os.environ["FMGI_NO_PLAN"] = "1"
+        try:
+            _compare_traces(example_scene, ctx, L, 41_000, 41_128, fmgi.KERNEL_HYBRID)
+            lm = _bake_gpu(torch_cuda, ctx, 40_000, 52_000, fmgi.KERNEL_HYBRID)
+            assert np.array_equal(lm[:, :3], olm), f"FMGI_NO_PLAN={env}"
+        finally:
+            os.environ.pop("FMGI_NO_PLAN", None)
+    ctx.close()
+
+
 ACCUMS = [fmgi.ACCUM_FX3, fmgi.ACCUM_STATE, fmgi.ACCUM_STREAM]
 
 
