@@ -20,6 +20,7 @@
  * Both kernels read the stream length from the device (no host round trip between bake and fold).
  */
 #include <hip/hip_runtime.h>
+#include <stdlib.h>
 
 #include "fmgi_internal.h"
 
@@ -160,6 +161,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
    its codes sorted by tile with the run offsets in toff, so one workgroup per (tile, group of segments)
    reads its tile's run of every segment directly. A wave takes 4 segments at a time, 16 lanes each
    (runs average FMGI_RING_CODES / P codes); the sums are k_tile_runs' (int64 R, G - R, B - R in LDS). */
+template <int SEG>
 __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restrict__ stream,
                                                        const uint16_t *__restrict__ toff,
                                                        const unsigned long long *__restrict__ n_ptr, uint64_t cap,
@@ -171,7 +173,8 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
     const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
     const int t = j % P, g = xcd + 8 * (j / P);
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
-    const uint64_t ns = n / FMGI_RING_CODES; /* reserved blocks are whole numbers of segments */
+    /* presorted: reserved blocks are whole numbers of segments; slice-sorted: the last slice is partial */
+    const uint64_t ns = SEG == FMGI_RING_CODES ? n / SEG : (n + SEG - 1) / SEG;
     const uint64_t s_lo = ns * g / G, s_hi = ns * (g + 1) / G;
     if (s_lo >= s_hi) return; /* uniform */
     for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
@@ -192,8 +195,8 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
             /* clamped to the segment: a block whose reservation failed (stream overflow, never by sizing;
                the call then reports the error) has no run table written, and its stale offsets must not
                send a read past the segment */
-            r0 = min((int)to[t], FMGI_RING_CODES);
-            len = max(0, min((int)to[t + 1], FMGI_RING_CODES) - r0);
+            r0 = min((int)to[t], SEG);
+            len = max(0, min((int)to[t + 1], SEG) - r0);
         }
     };
     int nr0, nlen;
@@ -208,15 +211,15 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
             if (lane >= d) pre += o;
         }
         const int total = __builtin_amdgcn_readlane(pre, kW - 1);
-        /* packed index i of run j (i in [start_j, start_j + len_j)) reads run_base + j*1024 + r0_j + i - start_j */
-        const int shift_l = lane * FMGI_RING_CODES + r0 - (pre - len);
+        /* packed index i of run j (i in [start_j, start_j + len_j)) reads run_base + j*SEG + r0_j + i - start_j */
+        const int shift_l = lane * SEG + r0 - (pre - len);
         int start[kW], shift[kW];
 #pragma unroll
         for (int j = 0; j < kW; j++) {
             start[j] = __builtin_amdgcn_readlane(pre - len, j);
             shift[j] = __builtin_amdgcn_readlane(shift_l, j);
         }
-        const uint32_t *run = stream + s0 * FMGI_RING_CODES;
+        const uint32_t *run = stream + s0 * SEG;
         for (int i0 = lane; i0 < total; i0 += 4 * 64) {
             uint32_t v[4];
 #pragma unroll
@@ -389,10 +392,10 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
         return hipGetLastError();
     }
     if (sb.presort) {
-        hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre, (int)plds);
+        hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre<FMGI_RING_CODES>, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
-        hipLaunchKernelGGL(k_tile_runs_pre, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
+        hipLaunchKernelGGL(k_tile_runs_pre<FMGI_RING_CODES>, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
                            sb.stream, sb.toff, sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
@@ -400,9 +403,21 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
     hipLaunchKernelGGL(k_slice_sort, dim3((unsigned)nslices), dim3(256), 0, s, sb.stream, sb.cursor, sb.cap, P,
                        sb.sorted, sb.toff);
     const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 64 KiB: two workgroups per CU */
+    const int G = (sb.groups + 7) & ~7; /* a multiple of 8 for the XCD-aware order */
+    /* a slice's run of one tile averages 8192 / P codes: past 128 tiles (runs of < 64) a wave packs 16
+       slices' runs onto its lanes (k_tile_runs_pre over slices), below it takes one run at a time
+       (FMGI_PACKED_RUNS=0/1 forces either, experiments) */
+    bool packed = P > 128;
+    if (const char *pe = getenv("FMGI_PACKED_RUNS")) packed = atoi(pe) != 0;
+    if (packed) {
+        hipError_t e = fmgi_set_lds_attr_once<4>((const void *)k_tile_runs_pre<kSlice>, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_tile_runs_pre<kSlice>, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), lds,
+                           s, sb.sorted, sb.toff, sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
+        return hipGetLastError();
+    }
     hipError_t e = fmgi_set_lds_attr_once<0>((const void *)k_tile_runs, (int)lds);
     if (e != hipSuccess) return e;
-    const int G = (sb.groups + 7) & ~7; /* a multiple of 8 for k_tile_runs' XCD-aware order */
     hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), lds, s, sb.sorted, sb.toff,
                        sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
     return hipGetLastError();

@@ -179,6 +179,14 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
         f.idx = i;
         cls[a][r.n.s[a] > 0 ? 0 : 1].push_back(f);
     }
+    /* each class nearest-first along the lanes that face it: the +a class (c = 0) is faced by rays going
+       -a, so it runs by descending plane, the -a class by ascending plane. A lane's fac' then never
+       decreases along the list once it is ahead of the lane, which lets the filter loop stop when every
+       lane of the wave is past its 2^-11 band (filter_axis). Same-plane records keep rect order. */
+    for (int a = 0; a < 3; a++) {
+        std::stable_sort(cls[a][0].begin(), cls[a][0].end(), [](const FilterRec &x, const FilterRec &y) { return x.plane > y.plane; });
+        std::stable_sort(cls[a][1].begin(), cls[a][1].end(), [](const FilterRec &x, const FilterRec &y) { return x.plane < y.plane; });
+    }
     FilterRec sentinel;
     memset(&sentinel, 0, sizeof sentinel);
     sentinel.hwu = -1.0f; /* |x| <= -1 is never true: a padding entry is never a candidate */
@@ -187,8 +195,12 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
     for (int a = 0; a < 3; a++) {
         fb.J[a] = (int)std::max(cls[a][0].size(), cls[a][1].size());
         for (int j = 0; j < fb.J[a]; j++)
-            for (int c = 0; c < 2; c++)
-                fb.img.push_back(j < (int)cls[a][c].size() ? cls[a][c][j] : sentinel);
+            for (int c = 0; c < 2; c++) {
+                /* a class's padding sits at the far end of its order (fac' = +inf for the lanes facing it) */
+                FilterRec pad = sentinel;
+                pad.plane = c == 0 ? -INFINITY : INFINITY;
+                fb.img.push_back(j < (int)cls[a][c].size() ? cls[a][c][j] : pad);
+            }
     }
     /* 8 padding pairs: a cooperative lane group reads up to coop - 1 records past the last class
        (k_bake, filter_axis) and discards them; they stay inside the staged image */
@@ -1170,12 +1182,16 @@ static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs,
 }
 
 /* the kernel instance a bake of `kernel` launches: the grid scan of a closed box (one plane per axis and
-   class) has its own instance (FMGI_KVAR_AXES); FMGI_NO_AXES (experiments) keeps the general one */
+   class) has its own instance (FMGI_KVAR_AXES); FMGI_NO_AXES (experiments) keeps the general one.
+   FMGI_PLAN=1 (experiments) walks the hybrid scan's walls over the floor plan: exact, but its per-lane
+   walks diverge and wait on dependent LDS reads, and example.png baked 2x slower than with the filter
+   pass (profiles/r03/s9) */
 static bool grid_axes_scene(const fmgi_context *c) {
     return c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES");
 }
 static int kernel_instance(const fmgi_context *c, int kernel) {
-    if (kernel == FMGI_KERNEL_HYBRID && c->plan_off >= 0 && !getenv("FMGI_NO_PLAN")) return kernel | FMGI_KVAR_PLAN;
+    const char *pe = getenv("FMGI_PLAN");
+    if (kernel == FMGI_KERNEL_HYBRID && c->plan_off >= 0 && pe && atoi(pe) == 1) return kernel | FMGI_KVAR_PLAN;
     return kernel == FMGI_KERNEL_GRID && grid_axes_scene(c) ? (kernel | FMGI_KVAR_AXES) : kernel;
 }
 

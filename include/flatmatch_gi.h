@@ -281,7 +281,7 @@ int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);
 int fmgi_get_stage_cycles(fmgi_context *ctx, uint64_t out[16]);
 int fmgi_grid_copy(const fmgi_context *ctx, void *planes, void *cells, float *recs, int32_t *idx);
 /* FMGI_KERNEL_HYBRID's floor plan of the walls (built by fmgi_set_scene; host-only contexts too; the
-   hybrid scan walks it unless FMGI_NO_PLAN is set): *bytes = its size (0: no plan for this scene); with
+   hybrid scan walks it with FMGI_PLAN=1): *bytes = its size (0: no plan for this scene); with
    blob != NULL and *bytes >= that size, copies it: {float x0, y0, 1 / cs, cs}, {int32 nx | ny << 16,
    ncells, nentries, 0}, u16 start[ncells + 1], u16 entry[nentries] (cell (ix, iy) = iy * nx + ix lists
    entry[start[i] .. start[i + 1]]: 32-B records of the filter image, record r at byte 32 r; x walls

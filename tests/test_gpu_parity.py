@@ -117,22 +117,22 @@ def test_box_traces_without_axes_mode(torch_cuda, box200, offsets):
         os.environ.pop("FMGI_NO_AXES", None)
 
 
-def test_layout_traces_without_floor_plan(torch_cuda, example_scene, offsets):
-    """The hybrid scan walks the floor plan of the walls (plan_walls); FMGI_NO_PLAN=1 runs its filter pass
-    over every wall instead: both give the oracle's traces and lightmap."""
+def test_layout_traces_with_floor_plan(torch_cuda, example_scene, offsets):
+    """The hybrid scan's walls through its filter pass (default: nearest-first classes, wave-uniform early
+    exit) and through the floor-plan walk (FMGI_PLAN=1, plan_walls): both give the oracle's traces and
+    lightmap."""
     spa = 6_500_000
     L = _oracle_plan(example_scene, spa, offsets)
     ctx = _ctx(example_scene, spa, offsets)
     olm, _ = O.bake(example_scene, L, 40_000, 52_000)
     for env in ("0", "1"):
-        if env == "1":
-            os.environ["FMGI_NO_PLAN"] = "1"
+        os.environ["FMGI_PLAN"] = env
         try:
             _compare_traces(example_scene, ctx, L, 41_000, 41_128, fmgi.KERNEL_HYBRID)
             lm = _bake_gpu(torch_cuda, ctx, 40_000, 52_000, fmgi.KERNEL_HYBRID)
-            assert np.array_equal(lm[:, :3], olm), f"FMGI_NO_PLAN={env}"
+            assert np.array_equal(lm[:, :3], olm), f"FMGI_PLAN={env}"
         finally:
-            os.environ.pop("FMGI_NO_PLAN", None)
+            os.environ.pop("FMGI_PLAN", None)
     ctx.close()
 
 
@@ -171,12 +171,15 @@ def test_lightmap_box_prefix_exact(torch_cuda, box200, box2000, offsets, kernel,
         ctx.close()
 
 
-@pytest.mark.parametrize("presort", ["1", "0"])
-def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, presort):
-    """The STREAM fold from the bake-side presorted segments (FMGI_PRESORT=1, the default for lightmaps of
-    at most 63 fold tiles) and from the slice-sorted stream (FMGI_PRESORT=0) give the oracle's lightmap,
-    for full-ring flushes and for the partial rings at the end of a launch."""
+@pytest.mark.parametrize("presort,packed", [("2", None), ("1", None), ("0", "0"), ("0", "1")])
+def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, presort, packed):
+    """The STREAM fold from the bake's per-tile buckets (FMGI_PRESORT=2, the default for lightmaps of at
+    most 63 fold tiles), from the bake-side presorted segments (1) and from the slice-sorted stream (0;
+    its runs summed one at a time, or packed 16 slices to a wave as for lightmaps of more than 128 tiles)
+    give the oracle's lightmap, for full-ring flushes and for the partial rings at the end of a launch."""
     os.environ["FMGI_PRESORT"] = presort
+    if packed is not None:
+        os.environ["FMGI_PACKED_RUNS"] = packed
     try:
         for sc, spa, lo, hi in ((box200, 172_413_793, 7_000, 27_000), (example_scene, 65_000, 0, 300)):
             L = _oracle_plan(sc, spa, offsets)
@@ -188,6 +191,7 @@ def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, pr
             ctx.close()
     finally:
         os.environ.pop("FMGI_PRESORT", None)
+        os.environ.pop("FMGI_PACKED_RUNS", None)
 
 
 def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets):

@@ -52,6 +52,10 @@ def _wall_records(sc, grid):
         nz = np.nonzero(n[i])[0]
         a = int(nz[0])
         cls[(a, 0 if n[i][a] > 0 else 1)].append(i)
+    # build_filter orders each class nearest-first for the lanes facing it: +n by descending plane, -n by
+    # ascending plane (stable: rect order within a plane)
+    for (a, c), lst in cls.items():
+        lst.sort(key=lambda i: -vals[i][0] if c == 0 else vals[i][0])
     J0 = max(len(cls[(0, 0)]), len(cls[(0, 1)]))
     recs = {}
     for a in (0, 1):

@@ -9,6 +9,8 @@ for f in sorted(glob.glob(os.path.join(sys.argv[1], "*.log"))):
     for line in open(f):
         if line.startswith("{"):
             d = json.loads(line)
+            if not isinstance(d.get("config"), dict):
+                continue
             r = d.get("roofline", {})
             print(f"{os.path.basename(f)[:-4]:14s} {d['config'].get('scene', '?'):12s} {d['value']:.4g} "
                   f"ms/step {d['ms_per_step']:.2f} bake {r.get('kernel_ms', 0):.2f} fold {r.get('fold_ms_per_step', 0):.2f} "
