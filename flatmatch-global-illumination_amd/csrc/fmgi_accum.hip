@@ -312,48 +312,102 @@ __global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ block_len,
                                                      const uint32_t *__restrict__ counts, int P, int G,
-                                                     const uint4 *__restrict__ colpack,
+                                                     int balanced, const uint4 *__restrict__ colpack,
                                                      unsigned long long *__restrict__ lm, int num_texels) {
     constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
     unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
-    const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
-    const int t = j % P, g = xcd + 8 * (j / P);
-    uint32_t off = 0;
-    for (int u = 0; u < t; u++) off += counts[u];
-    const uint32_t nt = counts[t];
-    const uint32_t j_lo = (uint32_t)((uint64_t)nt * g / G), j_hi = (uint32_t)((uint64_t)nt * (g + 1) / G);
+    uint32_t t = 0, off = 0, nt = 0, j_lo = 0, j_hi = 0;
+    if (balanced) {
+        /* the P * G workgroups shared out in proportion to the tiles' block counts (at least one each):
+           tile t owns workgroups [c(t), c(t + 1)) with c(t) = t + floor((W - P) * blocks before t / all),
+           so every workgroup folds about the same number of blocks whatever the tiles' sizes */
+        const uint32_t W = (uint32_t)(P * G), w = blockIdx.x;
+        uint64_t total = 0;
+        for (int u = 0; u < P; u++) total += counts[u];
+        if (total == 0) return;
+        uint64_t cum = 0;
+        uint32_t c0 = 0, c1 = 0;
+        for (int u = 0; u < P; u++) {
+            c0 = (uint32_t)u + (uint32_t)((uint64_t)(W - P) * cum / total);
+            c1 = (uint32_t)u + 1 + (uint32_t)((uint64_t)(W - P) * (cum + counts[u]) / total);
+            if (w < c1 || u == P - 1) {
+                t = (uint32_t)u;
+                break;
+            }
+            cum += counts[u];
+        }
+        off = (uint32_t)cum;
+        nt = counts[t];
+        const uint32_t wt = c1 - c0, g = w - c0;
+        if (w >= c1) return; /* uniform */
+        j_lo = (uint32_t)((uint64_t)nt * g / wt);
+        j_hi = (uint32_t)((uint64_t)nt * (g + 1) / wt);
+    } else {
+        const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
+        t = (uint32_t)(j % P);
+        const uint32_t g = (uint32_t)(xcd + 8 * (j / P));
+        for (uint32_t u = 0; u < t; u++) off += counts[u];
+        nt = counts[t];
+        j_lo = (uint32_t)((uint64_t)nt * g / G);
+        j_hi = (uint32_t)((uint64_t)nt * (g + 1) / G);
+    }
     if (j_lo >= j_hi) return; /* uniform */
     for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
     for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int waves = blockDim.x >> 6;
-    for (uint32_t jj = j_lo + wave; jj < j_hi; jj += waves) {
-        const uint32_t b = list[off + jj];
-        const uint32_t len = min(block_len[b], BP);
-        const uint4 *blk = (const uint4 *)(pool + (uint64_t)b * BP);
-        uint4 q[4];
-#pragma unroll
-        for (int u = 0; u < 4; u++) { /* 16-B unit i4 = 64 u + lane: codes 4 i4 .. 4 i4 + 3 */
-            const uint32_t i4 = 64 * u + lane;
-            q[u] = 4 * i4 < len ? blk[i4] : make_uint4(kSentinel, kSentinel, kSentinel, kSentinel);
+    /* the wave's blocks are j_lo + wave + k * waves: lane k holds block k's pool index and length (one
+       load each for up to 64 blocks at a time), so the loop reads them with readlane instead of two
+       dependent loads per block, and the next block's four 16-B loads are in flight while this block's
+       codes are summed */
+    const uint32_t span = j_hi - j_lo;
+    const uint32_t nb = span > (uint32_t)wave ? (span - (uint32_t)wave + waves - 1) / waves : 0u;
+    const uint4 sent4 = make_uint4(kSentinel, kSentinel, kSentinel, kSentinel);
+    for (uint32_t k0 = 0; k0 < nb; k0 += 64) {
+        const uint32_t kn = min(nb - k0, 64u);
+        uint32_t lb = 0, ll = 0;
+        if ((uint32_t)lane < kn) {
+            lb = list[off + j_lo + wave + (k0 + lane) * waves];
+            ll = min(block_len[lb], BP);
         }
+        uint4 q[4];
+        uint32_t len = 0;
+        auto fetch = [&](uint32_t k, uint4 (&qq)[4], uint32_t &ln) {
+            const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)lb, (int)k);
+            ln = (uint32_t)__builtin_amdgcn_readlane((int)ll, (int)k);
+            const uint4 *blk = (const uint4 *)(pool + (uint64_t)b * BP);
 #pragma unroll
-        for (int u = 0; u < 4; u++) {
-            const uint32_t i0 = 4 * (64 * u + lane);
-            const uint32_t cs[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
-#pragma unroll
-            for (int m = 0; m < 4; m++) {
-                const uint32_t c = cs[m];
-                if (i0 + m >= len || c == kSentinel) continue; /* runs are padded to 4 codes */
-                const int tx = (int)((c >> 10) & (kTileTexels - 1));
-                const uint4 cc = col[c & 1023];
-                atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
-                if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
-                if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
+            for (int u = 0; u < 4; u++) { /* 16-B unit i4 = 64 u + lane: codes 4 i4 .. 4 i4 + 3 */
+                const uint32_t i4 = 64 * u + lane;
+                qq[u] = 4 * i4 < ln ? blk[i4] : sent4;
             }
+        };
+        fetch(0, q, len);
+        for (uint32_t k = 0; k < kn; k++) {
+            uint4 qn[4] = {sent4, sent4, sent4, sent4};
+            uint32_t lenn = 0;
+            if (k + 1 < kn) fetch(k + 1, qn, lenn);
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const uint32_t i0 = 4 * (64 * u + lane);
+                const uint32_t cs[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+#pragma unroll
+                for (int m = 0; m < 4; m++) {
+                    const uint32_t c = cs[m];
+                    if (i0 + m >= len || c == kSentinel) continue; /* runs are padded to 4 codes */
+                    const int tx = (int)((c >> 10) & (kTileTexels - 1));
+                    const uint4 cc = col[c & 1023];
+                    atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
+                    if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
+                    if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
+                }
+            }
+#pragma unroll
+            for (int u = 0; u < 4; u++) q[u] = qn[u];
+            len = lenn;
         }
     }
     __syncthreads();
@@ -386,9 +440,11 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
         e = fmgi_set_lds_attr_once<3>((const void *)k_bucket_fold, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
+        const char *be = getenv("FMGI_FOLD_BALANCE"); /* experiments: 0 = equal groups per tile */
+        const int balanced = be ? atoi(be) != 0 : 1;
         hipLaunchKernelGGL(k_bucket_fold, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
-                           sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G, (const uint4 *)sb.colpack, lm,
-                           num_texels);
+                           sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G, balanced,
+                           (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
     if (sb.presort) {

@@ -117,6 +117,7 @@ struct FilterBuild {
     float margin = 0;
     double scale = 1; /* B: scene scale the margin is derived from */
     std::vector<FilterRec> cls[3][2]; /* axis-aligned records by (axis, class), rect order */
+    std::vector<int> pos[3][2];       /* cls[a][c][i] is the class-c half of image pair pos[a][c][i] */
 };
 
 int nonzero_axis(const float *v) {
@@ -179,28 +180,24 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
         f.idx = i;
         cls[a][r.n.s[a] > 0 ? 0 : 1].push_back(f);
     }
-    /* each class nearest-first along the lanes that face it: the +a class (c = 0) is faced by rays going
-       -a, so it runs by descending plane, the -a class by ascending plane. A lane's fac' then never
-       decreases along the list once it is ahead of the lane, which lets the filter loop stop when every
-       lane of the wave is past its 2^-11 band (filter_axis). Same-plane records keep rect order. */
-    for (int a = 0; a < 3; a++) {
-        std::stable_sort(cls[a][0].begin(), cls[a][0].end(), [](const FilterRec &x, const FilterRec &y) { return x.plane > y.plane; });
-        std::stable_sort(cls[a][1].begin(), cls[a][1].end(), [](const FilterRec &x, const FilterRec &y) { return x.plane < y.plane; });
-    }
     FilterRec sentinel;
     memset(&sentinel, 0, sizeof sentinel);
     sentinel.hwu = -1.0f; /* |x| <= -1 is never true: a padding entry is never a candidate */
     sentinel.hwv = -1.0f;
     sentinel.idx = -1;
+    /* pair j = {record j of the +a class, record j of the -a class}, rect order. (Measured and dropped,
+       profiles/r03/s10-s12: each class nearest-first with a wave-uniform early exit, 22.4 -> 31.6 ms on
+       example.png; the two faces of a wall paired, pairs in Morton order, chunks of 4 culled against the
+       box of the wave's ray segments, 29.8 ms: 64 random directions span the plan, nothing was culled,
+       and both loops lost the filter's 4-deep LDS pipelining) */
     for (int a = 0; a < 3; a++) {
         fb.J[a] = (int)std::max(cls[a][0].size(), cls[a][1].size());
+        for (int c = 0; c < 2; c++) {
+            fb.pos[a][c].resize(cls[a][c].size());
+            for (size_t i = 0; i < cls[a][c].size(); i++) fb.pos[a][c][i] = (int)i;
+        }
         for (int j = 0; j < fb.J[a]; j++)
-            for (int c = 0; c < 2; c++) {
-                /* a class's padding sits at the far end of its order (fac' = +inf for the lanes facing it) */
-                FilterRec pad = sentinel;
-                pad.plane = c == 0 ? -INFINITY : INFINITY;
-                fb.img.push_back(j < (int)cls[a][c].size() ? cls[a][c][j] : pad);
-            }
+            for (int c = 0; c < 2; c++) fb.img.push_back(j < (int)cls[a][c].size() ? cls[a][c][j] : sentinel);
     }
     /* 8 padding pairs: a cooperative lane group reads up to coop - 1 records past the last class
        (k_bake, filter_axis) and discards them; they stay inside the staged image */
@@ -430,11 +427,10 @@ PlanBuild build_plan(const FilterBuild &fb, const fmgi_rect *srcs, int ns) {
     struct Seg { double a_lo, a_hi, b_lo, b_hi; int r; }; /* footprint box in (x, y) and record index */
     std::vector<Seg> segs;
     for (int a = 0; a < 2; a++)
-        for (int j = 0; j < fb.J[a]; j++)
-            for (int c = 0; c < 2; c++) {
-                if (j >= (int)fb.cls[a][c].size()) continue;
+        for (int c = 0; c < 2; c++)
+            for (int j = 0; j < (int)fb.cls[a][c].size(); j++) {
                 const FilterRec &f = fb.cls[a][c][j];
-                const int r = 2 * ((a == 0 ? 0 : fb.J[0]) + j) + c;
+                const int r = 2 * ((a == 0 ? 0 : fb.J[0]) + fb.pos[a][c][j]) + c;
                 const double lo_u = (double)f.cu - f.hwu, hi_u = (double)f.cu + f.hwu;
                 /* x-walls (a = 0): x = plane, y = u; y-walls: y = plane, x = u */
                 if (a == 0) segs.push_back({f.plane, f.plane, lo_u, hi_u, r});
@@ -591,6 +587,7 @@ struct fmgi_context {
     int grid_cells = 0, grid_entries = 0;
     GridBuild h_grid; /* host copy (fmgi_grid_copy) */
     PlanBuild h_plan; /* ScanHybrid's floor plan of the walls (fmgi_plan_copy); h_plan.ok: built */
+    std::vector<FilterRec> h_fimg; /* the filter image (fmgi_filter_copy) */
     int plan_off = -1; /* its byte offset in the hybrid image */
     int auto_kernel = FMGI_KERNEL_FAST;
     /* optional device timing (fmgi_set_timing) */
@@ -957,6 +954,7 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     FilterBuild fb = build_filter(walls, num_walls, c->h_srcs.data(), (int)c->h_srcs.size());
     for (int a = 0; a < 3; a++) c->fJ[a] = fb.J[a];
     c->fimg_bytes = (int)(fb.img.size() * sizeof(FilterRec));
+    c->h_fimg = fb.img;
     c->ngeneral = (int)fb.general.size();
     c->margin = fb.margin;
     GridBuild gb = build_grid(fb);
@@ -1706,6 +1704,16 @@ FMGI_API int fmgi_grid_sizes(const fmgi_context *c, int32_t sizes[5]) {
     for (int a = 0; a < 3; a++) sizes[a] = c->h_grid.J[a];
     sizes[3] = (int32_t)c->h_grid.cells.size();
     sizes[4] = (int32_t)c->h_grid.idx.size();
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_filter_copy(const fmgi_context *c, void *img, int32_t *bytes, int32_t pairs[3]) {
+    if (!c || !bytes || !pairs) return set_err(FMGI_ERR_ARG, "fmgi_filter_copy: bad arguments");
+    const int32_t n = (int32_t)(c->h_fimg.size() * sizeof(FilterRec));
+    if (img && *bytes < n) return set_err(FMGI_ERR_ARG, "fmgi_filter_copy: buffer too small");
+    if (img && n) memcpy(img, c->h_fimg.data(), (size_t)n);
+    *bytes = n;
+    for (int a = 0; a < 3; a++) pairs[a] = c->fJ[a];
     return FMGI_OK;
 }
 

@@ -220,7 +220,7 @@ struct ScanExact {
 template <int A>
 __device__ __forceinline__ float comp(f3 v) { return A == 0 ? v.x : (A == 1 ? v.y : v.z); }
 
-template <int A, bool Coop, bool Exit = false>
+template <int A, bool Coop>
 __device__ __forceinline__ void filter_axis(const char *img, int J, int sub, int coop, f3 s, f3 d, float &L1,
                                             float &L2, int &code1) {
     constexpr int U = (A == 0) ? 1 : 0;
@@ -248,11 +248,6 @@ __device__ __forceinline__ void filter_axis(const char *img, int J, int sub, int
         L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
         code1 = lt ? ((A << 16) | j) : code1;
         L1 = lt ? key : L1;
-        /* Exit: each class runs nearest-first for the lanes facing it (fmgi_api.cpp build_filter), so
-           once this record's fac' is past the 2^-11 band above L1, every later one is too, and none can
-           win or change the separation test (grid_phase1_sorted's argument); the wave leaves the
-           uniform loop when all its lanes are there (checked every 4 records) */
-        if (Exit && (t & 3) == 3 && __all(!(f <= L1 * 1.00048828125f))) break;
     }
 }
 
@@ -283,15 +278,9 @@ struct ScanFastT {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         const int coop = Coop ? a.coop : 1, sub = Coop ? (int)__lane_id() & (coop - 1) : 0;
-        if (Coop) {
-            filter_axis<0, Coop>(lds, a.fJ[0], sub, coop, src, dir, L1, L2, code1);
-            filter_axis<1, Coop>(lds + 64 * a.fJ[0], a.fJ[1], sub, coop, src, dir, L1, L2, code1);
-            filter_axis<2, Coop>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], sub, coop, src, dir, L1, L2, code1);
-        } else { /* floors and ceilings first: they bound most rays, so the wall lists can stop early */
-            filter_axis<2, false, true>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], 0, 1, src, dir, L1, L2, code1);
-            filter_axis<0, false, true>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
-            filter_axis<1, false, true>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
-        }
+        filter_axis<0, Coop>(lds, a.fJ[0], sub, coop, src, dir, L1, L2, code1);
+        filter_axis<1, Coop>(lds + 64 * a.fJ[0], a.fJ[1], sub, coop, src, dir, L1, L2, code1);
+        filter_axis<2, Coop>(lds + 64 * (a.fJ[0] + a.fJ[1]), a.fJ[2], sub, coop, src, dir, L1, L2, code1);
         /* rects that are not axis-aligned: exact order-independent tests (no early-out); coop lanes split
            them like the filter records (each tested by one sub-lane, so coop_merge's L2 is the true
            runner-up and a winning general rect does not look tied with itself) */
@@ -795,8 +784,8 @@ struct ScanHybridT {
         if (Plan) { /* the walls the ray's floor-plan cells list, nearest cells first, after the floors */
             plan_walls(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
-            filter_axis<0, false, true>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
-            filter_axis<1, false, true>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
+            filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
+            filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
             ntest += (unsigned)(a.fJ[0] + a.fJ[1]);
         }
         cptr<int32_t> G = (cptr<int32_t>)a.general;

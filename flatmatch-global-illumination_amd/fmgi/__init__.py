@@ -222,6 +222,17 @@ class Context:
                 "ny": int(h1[0]) >> 16, "start": u16[: ncells + 1].copy(),
                 "entry": u16[ncells + 1 : ncells + 1 + nent].copy()}
 
+    def filter_image(self) -> dict:
+        """The filter image (include/flatmatch_gi.h fmgi_filter_copy): records [n, 8] as float32 (idx in
+        column 5 as int32 bits) and the pairs per axis."""
+        n = C.c_int32(0)
+        J = np.zeros(3, np.int32)
+        check(self.lib.fmgi_filter_copy(self.h, None, C.byref(n), _ptr(J)), "fmgi_filter_copy")
+        img = np.zeros(n.value // 4, np.float32)
+        check(self.lib.fmgi_filter_copy(self.h, _ptr(img), C.byref(n), _ptr(J)), "fmgi_filter_copy")
+        recs = img.reshape(-1, 8)
+        return {"J": [int(x) for x in J], "recs": recs, "idx": recs[:, 5].view(np.int32).copy()}
+
     def device_sincosf(self, x: np.ndarray, library: bool = False):
         """The samplers' sin/cos on the device (the restatement), or with library=True the device
         library's sinf/cosf that it restates."""

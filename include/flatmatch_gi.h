@@ -287,6 +287,12 @@ int fmgi_grid_copy(const fmgi_context *ctx, void *planes, void *cells, float *re
    entry[start[i] .. start[i + 1]]: 32-B records of the filter image, record r at byte 32 r; x walls
    first, r & 1 = the class, +n = 0). */
 int fmgi_plan_copy(const fmgi_context *ctx, void *blob, int32_t *bytes);
+/* The filter image of FMGI_KERNEL_FAST / HYBRID (built by fmgi_set_scene; host-only contexts too): pairs[a]
+   = its pairs on axis a; *bytes = its size; with img != NULL and *bytes >= that size, copies it: per axis,
+   pairs[a] pairs {record of the +n class, record of the -n class}, then 16 padding records; a record is
+   {float plane, cu, hwu, cv, hwv; int32 rect index (-1: padding); pad[2]} (32 B; extents grown by the
+   filter margin). Pair j holds record j of each class, rect order. */
+int fmgi_filter_copy(const fmgi_context *ctx, void *img, int32_t *bytes, int32_t pairs[3]);
 
 /* Host helpers exported for tests (no device needed). */
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);

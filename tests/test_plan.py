@@ -26,43 +26,20 @@ def _fma(a, b, c):
 def _tables(sc):
     ctx = fmgi.Context(-1)
     ctx.set_scene(sc)
-    plan, grid = ctx.plan_tables(), ctx.grid_tables()
+    plan, fimg = ctx.plan_tables(), ctx.filter_image()
     ctx.close()
-    return plan, grid
+    return plan, fimg
 
 
-def _wall_records(sc, grid):
-    """record index r of the filter image -> (axis, class, plane, cu, hwu, cv, hwv), as build_filter makes
-    them (the values come from the grid tables, which hold the same margin-grown records)"""
-    vals = {}
-    for p in grid["planes"]:
-        if np.isnan(p["plane"]):
-            continue
-        n = int(p["nu"]) * int(p["nv"])
-        for c in grid["cells"][p["cell_off"] : p["cell_off"] + n]:
-            for k, rec in ((0, c["r0"]), (1, c["r1"])):
-                if k < int(c["count"]):
-                    vals[int(c["idx0"] if k == 0 else c["idx1"])] = (F(p["plane"]),) + tuple(F(x) for x in rec)
-            rest = slice(int(c["rest"]), int(c["rest"]) + max(int(c["count"]) - 2, 0))
-            for rec, i in zip(grid["recs"][rest], grid["idx"][rest]):
-                vals[int(i)] = (F(p["plane"]),) + tuple(F(x) for x in rec)
-    n = sc.walls["n"][:, :3]
-    cls = {(a, c): [] for a in range(3) for c in range(2)}
-    for i in range(len(sc.walls)):
-        nz = np.nonzero(n[i])[0]
-        a = int(nz[0])
-        cls[(a, 0 if n[i][a] > 0 else 1)].append(i)
-    # build_filter orders each class nearest-first for the lanes facing it: +n by descending plane, -n by
-    # ascending plane (stable: rect order within a plane)
-    for (a, c), lst in cls.items():
-        lst.sort(key=lambda i: -vals[i][0] if c == 0 else vals[i][0])
-    J0 = max(len(cls[(0, 0)]), len(cls[(0, 1)]))
+def _wall_records(sc, fimg):
+    """record index r of the filter image -> (axis, class, plane, cu, hwu, cv, hwv) for every wall record"""
+    J0, J1 = fimg["J"][0], fimg["J"][1]
     recs = {}
-    for a in (0, 1):
-        for c in (0, 1):
-            for j, i in enumerate(cls[(a, c)]):
-                r = 2 * ((0 if a == 0 else J0) + j) + c
-                recs[r] = (a, c) + vals[i]
+    for r in range(2 * (J0 + J1)):
+        if fimg["idx"][r] < 0:
+            continue
+        q = fimg["recs"][r]
+        recs[r] = (0 if r < 2 * J0 else 1, r & 1) + tuple(F(x) for x in q[:5])
     return recs, J0
 
 

@@ -12,7 +12,8 @@
 #   bench            python bench.py $BENCH_ARGS
 #   env_<tag>        bench.py (no CPU legs) under the environment assignments in $ENV_<TAG>
 #   ab               bench.py (no CPU legs) with each experiment build in $AB_LIBS (FMGI_LIB), then the default build
-#   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3")
+#   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3"), under the
+#                    environment assignments in $ENVB_<TAG> if set
 #   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
 #   pmc              rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on a short bench ($PROF_ARGS)
 #   foldpmc          one rocprofv3 --pmc pass of LDS-pipe counters (the fold kernels' binding resource)
@@ -50,7 +51,8 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     ab)    for v in ${AB_LIBS:-base}; do step "ab_$v" 600 env FMGI_LIB=$v python bench.py --no-cpu-baseline ${AB_ARGS:-}; done &&
            step ab_default 600 python bench.py --no-cpu-baseline ${AB_ARGS:-} ;;
     env_*) v="ENV_$(echo "${s#env_}" | tr a-z A-Z)"; step "$s" 600 env ${!v} python bench.py --no-cpu-baseline ${AB_ARGS:-} ;;
-    bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; step "$s" 600 python bench.py ${!v:-} ;;
+    bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; e="ENVB_$(echo "${s#bench_}" | tr a-z A-Z)"
+             step "$s" 600 env ${!e:-} python bench.py ${!v:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     pmclist) step pmclist 120 rocprofv3 -L ;;
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU -d "$OUT/sq1" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
