@@ -341,8 +341,10 @@ using ScanFastCoop = ScanFastT<true>;
 /* The kernel's cell of hit point (uh, vh) on plane record g (64 B, see GridPlane). */
 __device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, const float4 g2, float uh, float vh) {
     /* g0 = {plane, u0, v0, iu}, g1 = {iv, mu, mv, nu}, g2 = {nv, cell_off, -, -} */
-    const float tu = fminf(fmaxf((uh - g0.y) * g0.w, 0.0f), g1.y);
-    const float tv = fminf(fmaxf((vh - g0.z) * g1.x, 0.0f), g1.z);
+    /* clamp to [0, n - 1]: v_med3_f32 (fminf(fmaxf()) adds a canonicalising max); the same cell for
+       every non-NaN coordinate, and a NaN hit point passes no record test in any cell */
+    const float tu = __builtin_amdgcn_fmed3f((uh - g0.y) * g0.w, 0.0f, g1.y);
+    const float tv = __builtin_amdgcn_fmed3f((vh - g0.z) * g1.x, 0.0f, g1.z);
     return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)tv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)tu;
 }
 

@@ -15,6 +15,7 @@
 #   bench_<tag>      python bench.py with the args in $BENCH_<TAG> (e.g. BENCH_FX3="--accum fx3"), under the
 #                    environment assignments in $ENVB_<TAG> if set
 #   prof             rocprofv3 --kernel-trace --stats on a short bench ($PROF_ARGS)
+#   prof_<tag>       the same with the bench args in $PROF_<TAG>
 #   pmc              rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes on a short bench ($PROF_ARGS)
 #   foldpmc          one rocprofv3 --pmc pass of LDS-pipe counters (the fold kernels' binding resource)
 #   sq               two rocprofv3 --pmc passes of SQ instruction / wait counters ($PROF_ARGS)
@@ -53,6 +54,8 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     env_*) v="ENV_$(echo "${s#env_}" | tr a-z A-Z)"; step "$s" 600 env ${!v} python bench.py --no-cpu-baseline ${AB_ARGS:-} ;;
     bench_*) v="BENCH_$(echo "${s#bench_}" | tr a-z A-Z)"; e="ENVB_$(echo "${s#bench_}" | tr a-z A-Z)"
              step "$s" 600 env ${!e:-} python bench.py ${!v:-} ;;
+    prof_*) v="PROF_$(echo "${s#prof_}" | tr a-z A-Z)"
+            step "$s" 600 rocprofv3 --kernel-trace --stats -d "$OUT/$s" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${!v:-} ;;
     prof)  step prof 600 rocprofv3 --kernel-trace --stats -d "$OUT/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     pmclist) step pmclist 120 rocprofv3 -L ;;
     sq)    step sq1 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU -d "$OUT/sq1" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
