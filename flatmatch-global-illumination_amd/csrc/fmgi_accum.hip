@@ -32,47 +32,56 @@ constexpr uint32_t kSentinel = 0xFFFFFFFFu;
 
 __device__ __forceinline__ int tile_of(uint32_t code) { return (int)(code >> (10 + FMGI_TILE_BITS)); }
 
-/* exclusive scan of cnt[0..P) into loc[0..P) by one 256-thread block (P <= FMGI_MAX_TILES) */
+/* exclusive scan of cnt[0..P) into loc[0..P) by the first 256 threads of a block of NT >= 256 (P <=
+   FMGI_MAX_TILES); every thread of the block takes part in its barriers */
+template <int NT>
 __device__ void block_exclusive_scan(const uint32_t *cnt, uint32_t *loc, int P) {
     __shared__ uint32_t part[256];
     constexpr int per = FMGI_MAX_TILES / 256;
+    const bool in = NT == 256 || threadIdx.x < 256;
     const int t0 = threadIdx.x * per;
     uint32_t s = 0;
-    for (int k = 0; k < per; k++) s += (t0 + k < P) ? cnt[t0 + k] : 0u;
-    part[threadIdx.x] = s;
+    if (in) {
+        for (int k = 0; k < per; k++) s += (t0 + k < P) ? cnt[t0 + k] : 0u;
+        part[threadIdx.x] = s;
+    }
     __syncthreads();
     for (int off = 1; off < 256; off <<= 1) { /* Hillis-Steele over the 256 partial sums */
-        const uint32_t v = threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
+        const uint32_t v = in && threadIdx.x >= (unsigned)off ? part[threadIdx.x - off] : 0u;
         __syncthreads();
-        part[threadIdx.x] += v;
+        if (in) part[threadIdx.x] += v;
         __syncthreads();
     }
-    uint32_t run = part[threadIdx.x] - s;
-    for (int k = 0; k < per; k++) {
-        if (t0 + k < P) {
-            loc[t0 + k] = run;
-            run += cnt[t0 + k];
+    if (in) {
+        uint32_t run = part[threadIdx.x] - s;
+        for (int k = 0; k < per; k++) {
+            if (t0 + k < P) {
+                loc[t0 + k] = run;
+                run += cnt[t0 + k];
+            }
         }
     }
     __syncthreads();
 }
 
-__global__ __launch_bounds__(256) void k_slice_sort(const uint32_t *__restrict__ stream,
-                                                   const unsigned long long *__restrict__ n_ptr, uint64_t cap,
-                                                   int P, uint32_t *__restrict__ sorted,
-                                                   uint16_t *__restrict__ toff) {
-    __shared__ uint32_t buf[kSlice];
+/* one block of NT threads per SL-code slice; the slice is staged in dynamic LDS (SL x 4 B) */
+template <int SL, int NT>
+__global__ __launch_bounds__(NT) void k_slice_sort(const uint32_t *__restrict__ stream,
+                                                  const unsigned long long *__restrict__ n_ptr, uint64_t cap,
+                                                  int P, uint32_t *__restrict__ sorted,
+                                                  uint16_t *__restrict__ toff) {
+    extern __shared__ uint32_t buf[];
     __shared__ uint32_t cnt[FMGI_MAX_TILES], loc[FMGI_MAX_TILES];
-    constexpr int per = kSlice / 256;
+    constexpr int per = SL / NT;
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
-    const uint64_t b0 = (uint64_t)blockIdx.x * kSlice;
+    const uint64_t b0 = (uint64_t)blockIdx.x * SL;
     if (b0 >= n) return; /* uniform: the whole slice is past the end of the stream */
     for (int i = threadIdx.x; i < P; i += blockDim.x) cnt[i] = 0;
     __syncthreads();
     uint32_t c[per];
 #pragma unroll
     for (int k = 0; k < per; k++) { /* all loads in flight before the first LDS atomic */
-        const uint64_t i = b0 + (uint64_t)k * 256 + threadIdx.x;
+        const uint64_t i = b0 + (uint64_t)k * NT + threadIdx.x;
         c[k] = i < n ? stream[i] : kSentinel;
         /* a code of a tile >= P is never written by the bake; only the unwritten part of a block whose
            reservation failed (stream overflow, reported by the call) can hold one: dropped */
@@ -82,7 +91,7 @@ __global__ __launch_bounds__(256) void k_slice_sort(const uint32_t *__restrict__
     for (int k = 0; k < per; k++)
         if (c[k] != kSentinel) atomicAdd(&cnt[tile_of(c[k])], 1u);
     __syncthreads();
-    block_exclusive_scan(cnt, loc, P);
+    block_exclusive_scan<NT>(cnt, loc, P);
     uint16_t *to = toff + (size_t)blockIdx.x * (P + 1);
     for (int i = threadIdx.x; i < P; i += blockDim.x) {
         to[i] = (uint16_t)loc[i];
@@ -157,11 +166,13 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
     }
 }
 
-/* The fold of a presorted stream (BakeArgs::presort): every FMGI_RING_CODES-code segment already holds
-   its codes sorted by tile with the run offsets in toff, so one workgroup per (tile, group of segments)
-   reads its tile's run of every segment directly. A wave takes 4 segments at a time, 16 lanes each
-   (runs average FMGI_RING_CODES / P codes); the sums are k_tile_runs' (int64 R, G - R, B - R in LDS). */
-template <int SEG>
+/* The fold of a presorted stream (BakeArgs::presort): every SEG-code segment already holds its codes
+   sorted by tile with the run offsets in toff, so one workgroup per (tile, group of segments) reads its
+   tile's run of every segment directly. A wave takes kW segments at a time and packs their runs onto its
+   lanes (runs average SEG / P codes: kW = 16 for the bake's 1024-code segments, 4 for 32768-code slices,
+   whose runs are 4x longer and whose packed index costs kW - 1 compares per code); the sums are
+   k_tile_runs' (int64 R, G - R, B - R in LDS). */
+template <int SEG, int kW>
 __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restrict__ stream,
                                                        const uint16_t *__restrict__ toff,
                                                        const unsigned long long *__restrict__ n_ptr, uint64_t cap,
@@ -187,7 +198,6 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
        group's run bounds are loaded before this group's codes are folded. */
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int waves = blockDim.x >> 6;
-    constexpr int kW = 16;
     auto bounds = [&](uint64_t s0, int &r0, int &len) {
         r0 = 0, len = 0;
         if (lane < kW && s0 + lane < s_hi) {
@@ -448,30 +458,37 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
         return hipGetLastError();
     }
     if (sb.presort) {
-        hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre<FMGI_RING_CODES>, (int)plds);
+        hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre<FMGI_RING_CODES, 16>, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
-        hipLaunchKernelGGL(k_tile_runs_pre<FMGI_RING_CODES>, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
+        hipLaunchKernelGGL((k_tile_runs_pre<FMGI_RING_CODES, 16>), dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
                            sb.stream, sb.toff, sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
-    const uint64_t nslices = (sb.cap + kSlice - 1) / kSlice;
-    hipLaunchKernelGGL(k_slice_sort, dim3((unsigned)nslices), dim3(256), 0, s, sb.stream, sb.cursor, sb.cap, P,
-                       sb.sorted, sb.toff);
     const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 64 KiB: two workgroups per CU */
     const int G = (sb.groups + 7) & ~7; /* a multiple of 8 for the XCD-aware order */
-    /* a slice's run of one tile averages 8192 / P codes: past 128 tiles (runs of < 64) a wave packs 16
-       slices' runs onto its lanes (k_tile_runs_pre over slices), below it takes one run at a time
-       (FMGI_PACKED_RUNS=0/1 forces either, experiments) */
+    /* a slice's run of one tile averages slice / P codes: past 128 tiles the slices are 32768 codes (runs
+       of ~90 at 358 tiles instead of ~23: the fold's per-run work and run-table reads shrink 4x; the sort
+       stays HBM-bound) and a wave packs 16 slices' runs onto its lanes (k_tile_runs_pre over slices);
+       below, 8192-code slices and one run at a time (FMGI_PACKED_RUNS=0/1 forces either, experiments) */
     bool packed = P > 128;
     if (const char *pe = getenv("FMGI_PACKED_RUNS")) packed = atoi(pe) != 0;
     if (packed) {
-        hipError_t e = fmgi_set_lds_attr_once<4>((const void *)k_tile_runs_pre<kSlice>, (int)lds);
+        constexpr int kBig = FMGI_STREAM_SLICE_BIG;
+        const uint64_t nslices = (sb.cap + kBig - 1) / kBig;
+        hipError_t e = fmgi_set_lds_attr_once<5>((const void *)k_slice_sort<kBig, 1024>, kBig * 4);
         if (e != hipSuccess) return e;
-        hipLaunchKernelGGL(k_tile_runs_pre<kSlice>, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), lds,
+        hipLaunchKernelGGL((k_slice_sort<kBig, 1024>), dim3((unsigned)nslices), dim3(1024), (size_t)kBig * 4, s,
+                           sb.stream, sb.cursor, sb.cap, P, sb.sorted, sb.toff);
+        e = fmgi_set_lds_attr_once<4>((const void *)k_tile_runs_pre<kBig, 4>, (int)lds);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL((k_tile_runs_pre<kBig, 4>), dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), lds,
                            s, sb.sorted, sb.toff, sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
+    const uint64_t nslices = (sb.cap + kSlice - 1) / kSlice;
+    hipLaunchKernelGGL((k_slice_sort<kSlice, 256>), dim3((unsigned)nslices), dim3(256), (size_t)kSlice * 4, s, sb.stream,
+                       sb.cursor, sb.cap, P, sb.sorted, sb.toff);
     hipError_t e = fmgi_set_lds_attr_once<0>((const void *)k_tile_runs, (int)lds);
     if (e != hipSuccess) return e;
     hipLaunchKernelGGL(k_tile_runs, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), lds, s, sb.sorted, sb.toff,

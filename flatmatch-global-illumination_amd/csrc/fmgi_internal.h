@@ -126,6 +126,8 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 #define FMGI_RING_CODES 1024   /* codes a wave collects in LDS before writing them out       */
 static_assert(FMGI_STREAM_BLOCK % FMGI_RING_CODES == 0, "ring flushes must tile the stream blocks");
 #define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
+#define FMGI_STREAM_SLICE_BIG 32768 /* ... for lightmaps of more than 128 fold tiles                */
+static_assert(FMGI_STREAM_SLICE_BIG % FMGI_STREAM_SLICE == 0, "run tables are sized for the small slices");
 #define FMGI_RING_PAD 192 /* the ring's overflow (< 64 codes) lies in the first 64 of these; the bucketed
                              stream sorts a flush into ring[0, RING + 3 * 63) (runs padded to 4 codes)   */
 #define FMGI_RING_HIST (FMGI_RING_CODES + FMGI_RING_PAD)      /* tile histogram (64)                     */

@@ -156,11 +156,12 @@ enum { FMGI_KERNEL_EXACT = 0, FMGI_KERNEL_FAST = 1, FMGI_KERNEL_GRID = 2, FMGI_K
    FX3   three int64 fixed-point atomics per deposit into the lightmap;
    STATE one u64 atomic per deposit into counts[colour state][texel] (8 KiB per texel of device memory),
          folded into the int64 lightmap at the end of every fmgi_bake_items;
-   STREAM no atomics per deposit: 32-bit codes (texel << 10 | colour state) appended with coalesced
-         stores (sorted by 2048-texel fold tile in each wave's LDS ring when the lightmap has at most 63
-         tiles), then summed per tile exactly in LDS (needs < 4,194,304 texels; the codes of a chunk of
-         work items stay in HBM, 3.2 KB per work item at most, chunks sized to half of the free device
-         memory: one 1e9-photon chunk on an MI355X);
+   STREAM no atomics per deposit: 32-bit codes (texel << 10 | colour state) collected in each wave's LDS
+         ring and written with 16-B stores (when the lightmap has at most 63 fold tiles of 2048 texels,
+         sorted by tile into per-wave, per-tile 4-KB buckets; else into plain blocks that a second pass
+         sorts per 8192-code slice), then summed per tile exactly in LDS (needs < 4,194,304 texels; the
+         codes of a chunk of work items stay in HBM, 3.2 KB per work item at most, chunks sized to half
+         of the free device memory: one 1e9-photon chunk on an MI355X);
    AUTO  STREAM when the texel count allows it, else FX3;
    NONE  PROFILING ONLY: deposits are discarded (measures the tracing work alone; wrong lightmap). */
 enum { FMGI_ACCUM_AUTO = 0, FMGI_ACCUM_FX3 = 1, FMGI_ACCUM_STATE = 2, FMGI_ACCUM_NONE = 3, FMGI_ACCUM_STREAM = 4 };
@@ -247,7 +248,8 @@ int fmgi_auto_kernel(const fmgi_context *ctx);
    by default. fmgi_get_timing synchronises, returns the sums since the previous call and resets them. */
 typedef struct {
     double bake_ms;         /* k_bake launches                                   */
-    double fold_ms;         /* STREAM fold (k_tile_runs_pre, or k_slice_sort + k_tile_runs) */
+    double fold_ms;         /* STREAM fold (k_bucket_count/list/fold, k_tile_runs_pre, or k_slice_sort +
+                               k_tile_runs / k_tile_runs_pre over slices) */
     uint64_t bake_launches;
     uint64_t fold_launches;
 } fmgi_timing;
