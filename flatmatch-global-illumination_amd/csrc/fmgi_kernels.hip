@@ -36,6 +36,16 @@ using cptr = const __attribute__((address_space(4))) T *; /* constant space: sca
 template <class T>
 using gptr = const __attribute__((address_space(1))) T *; /* global space: vector loads, never flat */
 
+/* A uniform kernel argument re-read where it is used: the empty volatile asm keeps the compiler from
+   hoisting the comparison out of the bake loop as a 64-bit lane mask (one per condition, held across
+   the loop: the masks were most of the SGPRs the register allocator spilled to VGPR lanes and read back
+   with v_readlane, a VALU instruction, on every use) */
+template <class T>
+__device__ __forceinline__ T uni(T v) {
+    asm volatile("" : "+s"(v));
+    return v;
+}
+
 struct LcgJumpC {
     uint32_t a[41], c[41];
 };
@@ -117,7 +127,7 @@ __device__ __forceinline__ float exact_hit_rec(const R &r, int idx, f3 src, f3 d
    staged it there (BakeArgs::rects_off >= 0), else from global memory; the two reads stay in their own address
    spaces (a pointer that may be either compiles to flat loads, which wait on both counters) */
 __device__ __forceinline__ float exact_hit(const BakeArgs &a, const char *lds, int idx, f3 src, f3 dir, HitRec &h) {
-    if (a.rects_off >= 0)
+    if (uni(a.rects_off) >= 0)
         return exact_hit_rec(((const __attribute__((address_space(3))) RectLds *)(
                                  (const __attribute__((address_space(3))) char *)lds + a.rects_off))[idx],
                              idx, src, dir, h);
@@ -187,7 +197,7 @@ struct ScanExact {
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         float bestd = INFINITY;
         int hit = -1;
-        for (int i = 0; i < a.nrects; i++) {
+        for (int i = 0; i < uni(a.nrects); i++) {
             const float d = Scalar ? exact_on(R, i, src, dir, bestd) : exact_on_v(a.rects, i, src, dir, bestd);
             if (d < 0) continue;
             if (d < bestd) { bestd = d; hit = i; }
@@ -627,10 +637,13 @@ struct ScanGridT {
         for (int round = 0; round < kOrderedRounds; round++) {
             int nxt = INT_MAX;
             auto take = [&](int idx) { nxt = (idx > prev && idx < nxt) ? idx : nxt; };
-            grid_visit<0>(a, lds, 0, a.fJ[0], src, dir, take);
-            grid_visit<1>(a, lds, 128 * a.fJ[0], a.fJ[1], src, dir, take);
-            grid_visit<2>(a, lds, 128 * (a.fJ[0] + a.fJ[1]), a.fJ[2], src, dir, take);
-            for (int g = 0; g < a.ngeneral; g++) {
+            /* the closed-box instance knows its plane counts ({1, 1, 1}): constants, not uniform masks
+               the register allocator would keep live across the bake loop */
+            const int J0 = Axes ? 1 : a.fJ[0], J1 = Axes ? 1 : a.fJ[1], J2 = Axes ? 1 : a.fJ[2];
+            grid_visit<0>(a, lds, 0, J0, src, dir, take);
+            grid_visit<1>(a, lds, 128 * J0, J1, src, dir, take);
+            grid_visit<2>(a, lds, 128 * (J0 + J1), J2, src, dir, take);
+            for (int g = 0; g < uni(a.ngeneral); g++) {
                 const int idx = a.general[g];
                 if (idx > prev && idx < nxt && exact_on_v(a.rects, idx, src, dir, INFINITY) >= 0) nxt = idx;
             }
@@ -670,7 +683,7 @@ struct ScanGridT {
             }
         }
         cptr<int32_t> G = (cptr<int32_t>)a.general;
-        for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
+        for (int g = 0; g < uni(a.ngeneral); g++) { /* not axis-aligned: exact order-independent tests */
             const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
@@ -791,7 +804,7 @@ struct ScanHybridT {
             ntest += (unsigned)(a.fJ[0] + a.fJ[1]);
         }
         cptr<int32_t> G = (cptr<int32_t>)a.general;
-        for (int g = 0; g < a.ngeneral; g++) { /* not axis-aligned: exact order-independent tests */
+        for (int g = 0; g < uni(a.ngeneral); g++) { /* not axis-aligned: exact order-independent tests */
             const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
@@ -915,7 +928,7 @@ struct AccStream {
         const uint64_t live = __ballot(true);
         const uint32_t nl = (uint32_t)__popcll(live);
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-        const int P = a.ntiles;
+        const int P = uni(a.ntiles);
         const uint32_t shift = 10 + FMGI_TILE_BITS;
         for (uint32_t k = r; k < 64; k += nl) hist[k] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -1085,7 +1098,7 @@ struct AccStream {
         const uint64_t live = __ballot(true);
         const uint32_t nl = (uint32_t)__popcll(live);
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
-        const int P = a.ntiles;
+        const int P = uni(a.ntiles);
         const uint32_t shift = 10 + FMGI_TILE_BITS;
         for (uint32_t t = r; t < 64; t += nl) hist[t] = 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
@@ -1192,8 +1205,9 @@ struct AccStream {
         ws.tot += n;
         if (fill + n < FMGI_RING_CODES) return;
         /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
-        if (a.presort == 2) bucket_out(a, ring, FMGI_RING_CODES);
-        else if (a.presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
+        const int presort = uni(a.presort);
+        if (presort == 2) bucket_out(a, ring, FMGI_RING_CODES);
+        else if (presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
         else copy_out(a, ws, ring, FMGI_RING_CODES);
         const uint32_t rest = fill + n - FMGI_RING_CODES; /* < n <= live lanes: one code per live lane */
         const uint64_t live = __ballot(true);
@@ -1250,15 +1264,22 @@ struct HasAppend<AccStream> {
    launch_cap = WG*100 items (global_illumination_cl.c:255), so one search over the (few) sources and a
    division replace a search over all launches */
 __device__ __forceinline__ void locate_item(const BakeArgs &a, uint64_t w, int &src, int &li, uint32_t &gid) {
-    int lo = 0, hi = a.nsrc - 1;
+    int lo = 0, hi = uni(a.nsrc) - 1;
     while (lo < hi) {
         const int mid = (lo + hi + 1) >> 1;
         if (a.src_item_begin[mid] <= w) lo = mid; else hi = mid - 1;
     }
     const uint64_t off = w - a.src_item_begin[lo];
     src = lo;
-    li = a.src_launch0[lo] + (int)(off / a.launch_cap);
-    gid = (uint32_t)(off % a.launch_cap);
+    const uint32_t cap = a.launch_cap;
+    if ((off >> 32) == 0) { /* every schedule here: a 32-bit division, not the 64-bit expansion */
+        const uint32_t o = (uint32_t)off, q = o / cap;
+        li = a.src_launch0[lo] + (int)q;
+        gid = o - q * cap;
+    } else {
+        li = a.src_launch0[lo] + (int)(off / cap);
+        gid = (uint32_t)(off % cap);
+    }
 }
 
 /* the emitter fields photon emission reads (photonmap.cl:173-181 and the sampler basis) */
@@ -1276,7 +1297,7 @@ __device__ __forceinline__ SrcDev src_fields(const R &r) {
 
 /* emitter srci: from the workgroup's LDS copy of the SrcDev table when staged (BakeArgs::srcs_off >= 0) */
 __device__ __forceinline__ SrcDev load_src(const BakeArgs &a, const char *lds, int srci) {
-    if (a.srcs_off >= 0)
+    if (uni(a.srcs_off) >= 0)
         return src_fields(((const __attribute__((address_space(3))) SrcDev *)(
             (const __attribute__((address_space(3))) char *)lds + a.srcs_off))[srci]);
     return src_fields(((gptr<SrcDev>)a.srcs)[srci]);
@@ -1345,7 +1366,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 /* the finished item's scans, per source (the host orders the next bake's fetches by them):
                    the lane's running scan count is added here and was subtracted at the item's fetch, so
                    no register holds the item's start count */
-                if (a.src_cost && lead && photon >= 0)
+                if (uni(a.src_cost) && lead && photon >= 0)
                     atomicAdd(a.src_cost + srci, (unsigned long long)(n_dep + n_esc));
                 if (sst.tests && lead) { /* flush this lane's rect-test count (see ScanStats) */
                     atomicAdd(a.stats + KSTAT_TESTS, (unsigned long long)sst.tests);
@@ -1355,7 +1376,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 uint64_t w = lead ? atomicAdd(a.counter, 1ull) : 0ull;
                 if (Scan::kCoop) w = __shfl(w, (int)__lane_id() & ~(a.coop - 1), 64);
                 if (w >= a.item_end - a.item_begin) break;
-                if (a.fetch_nseg > 0) { /* fetch order: segments of source ranges, costliest items first
+                if (uni(a.fetch_nseg) > 0) { /* fetch order: segments of source ranges, costliest items first
                                            (32-bit: the host builds a table only below 2^32 items) */
                     const uint32_t f = (uint32_t)w;
                     int lo = 0, hi = a.fetch_nseg - 1;
@@ -1371,7 +1392,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 int li;
                 uint32_t gid;
                 locate_item(a, w, srci, li, gid);
-                if (a.src_cost && lead) atomicAdd(a.src_cost + srci, 0ull - (unsigned long long)(n_dep + n_esc));
+                if (uni(a.src_cost) && lead) atomicAdd(a.src_cost + srci, 0ull - (unsigned long long)(n_dep + n_esc));
                 rng = gid + (uint32_t)a.launches[li].rng_offset; /* photonmap.cl:272 */
                 /* photonmap.cl:273-275: r = rand()*40; ceil(r) further draws, as one LCG jump */
                 const float r40 = rng_next(rng) * 40;

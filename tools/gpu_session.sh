@@ -1,6 +1,7 @@
 #!/usr/bin/env bash
 # One gpurun session. Steps (FMGI_STEPS, space separated):
 #   tests            pytest -m gpu
+#   smoke            __graft_entry__.smoke()
 #   tests_k          pytest -m gpu $TESTS_ARGS (e.g. '-k radiosity')
 #   rad / radprof    tools/bench_rad.py $RAD_ARGS (plain / under rocprofv3 --kernel-trace --stats)
 #   ref              reference-kernel pin (tests/golden/make_ref_fixtures.py)
@@ -39,6 +40,7 @@ export TMPDIR=/tmp
 for s in ${FMGI_STEPS:-tests ref bench prof}; do
   case $s in
     tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
     tests_k) step tests_k 900 python -m pytest -m gpu -q -x -p no:cacheprovider ${TESTS_ARGS:-tests} ;;
     rad)   step rad 900 python tools/bench_rad.py ${RAD_ARGS:-} ;;
     radprof) step radprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/radprof" -o run --output-format csv -- python tools/bench_rad.py --reps 1 --no-cpu-baseline ${RAD_ARGS:-} ;;
