@@ -829,6 +829,10 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     uint64_t entries = 0;
     if (mode == kStreamBuckets) {
         sb.pool_blocks = bucket_pool_blocks(cap, P, grid, block);
+        /* FMGI_POOL_LIMIT=n (tests): at most n pool blocks, so the bake runs out of them and takes the
+           exact atomic fallback (bucket_atomic) for the rest of its codes */
+        if (const char *pl = getenv("FMGI_POOL_LIMIT"))
+            if (atoll(pl) > 0) sb.pool_blocks = std::min<uint64_t>(sb.pool_blocks, (uint64_t)atoll(pl));
         entries = 3 * sb.pool_blocks * 2; /* three u32 arrays, in u16 units */
         if (!sb.tile_blocks) HIPCHK(hipMalloc(&sb.tile_blocks, 2 * (FMGI_PRESORT_MAX_TILES + 1) * sizeof(uint32_t)));
     } else {

@@ -194,6 +194,23 @@ def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, pr
         os.environ.pop("FMGI_PACKED_RUNS", None)
 
 
+def test_bucket_pool_exhaustion_falls_back_exactly(torch_cuda, box200, offsets):
+    """A bucketed stream whose pool runs out (FMGI_POOL_LIMIT caps it at 64 blocks, far fewer than the
+    bake needs) sends the rest of its codes through device atomics into the int64 lightmap
+    (AccStream::bucket_atomic): the lightmap still equals the oracle's."""
+    os.environ["FMGI_POOL_LIMIT"] = "64"
+    try:
+        spa = 172_413_793
+        L = _oracle_plan(box200, spa, offsets)
+        ctx = _ctx(box200, spa, offsets, fmgi.ACCUM_STREAM)
+        lm = _bake_gpu(torch_cuda, ctx, 2_000, 6_000, fmgi.KERNEL_AUTO)
+        olm, _ = O.bake(box200, L, 2_000, 6_000)
+        assert np.array_equal(lm[:, :3], olm)
+        ctx.close()
+    finally:
+        os.environ.pop("FMGI_POOL_LIMIT", None)
+
+
 def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets):
     """Config 3 sized work (a 1e8-photon slice): order-free exact accumulation means any split of the
     item range, and any repetition, gives identical bits."""
