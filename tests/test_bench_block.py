@@ -1,0 +1,50 @@
+"""CPU test of bench.py's roofline block over the committed measurement set (profiles/): every figure
+the BENCH line derives from counters can be recomputed from the files of this commit, and is bounded."""
+import importlib.util
+import json
+import os
+
+import pytest
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+def _bench():
+    spec = importlib.util.spec_from_file_location("bench_mod", os.path.join(REPO, "bench.py"))
+    m = importlib.util.module_from_spec(spec)
+    spec.loader.exec_module(m)
+    return m
+
+
+def test_issue_block_from_committed_counters_is_bounded():
+    b = _bench()
+    rec = b.sq_record("box200")
+    assert rec is not None, "profiles/sq_issue.json has no box200 record"
+    # the counters' own source directory is committed
+    src = rec["source"].split("/{")[0]
+    assert os.path.isdir(os.path.join(REPO, src)), src
+    kernel_s = json.load(open(os.path.join(REPO, src, "kernel_timed_launches.json")))["k_bake_timed_mean_ms"] / 1e3
+    scans = 8.0e9  # box200: scans per launch (bench per_photon.scans x photons)
+    iss = b.issue_block(rec, kernel_s, scans, 256)
+    assert iss is not None
+    for k in ("valu_frac_of_peak",):
+        assert 0 < iss[k] <= 1.05, (k, iss[k])
+    w = iss["wave_cycles"]
+    assert abs(w["issuing"] + w["issue_stalled"] + w["waiting"] - 1.0) < 0.02, w
+    for k, v in iss["vmem_path"].items():
+        if k.endswith("busy") or k.startswith("td_stalled"):
+            assert 0 <= v <= 1.0, (k, v)
+    assert 0 < iss["valu_per_simd_cycle"] <= 1.0
+    # the profiled launch (GRBM busy cycles at the in-kernel clock) agrees with the live HIP-event time
+    assert iss["profiled_launch_ms"] == pytest.approx(kernel_s * 1e3, rel=0.03)
+    bound, why = b.binding_of(iss, 0.0)
+    assert bound in ("valu", "vmem", "latency", "atomics") and why
+
+
+def test_traffic_summary_is_committed():
+    p = os.path.join(REPO, "profiles", "pmc_traffic.json")
+    d = json.load(open(p))["box200"]
+    assert "k_bake" in d["kernel"]
+    assert d["hbm_bytes_per_launch"] == pytest.approx(d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"])
+    src = d["source"].split(":")[0]
+    assert os.path.isdir(os.path.join(REPO, src)), src
