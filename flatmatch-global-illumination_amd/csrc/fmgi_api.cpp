@@ -859,7 +859,10 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     {
         const int ncu = std::max(1, c->num_cus);
         const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
-        const int rounds = mode != kStreamSliced ? 16 : 8;
+        /* bucketed: ~36 rounds (box200, 46 tiles: fold 11.22 / 10.86 / 10.92 / 11.19 / 12.70 ms at 96 / 200 /
+           300 / 800 / 1600 groups, profiles/r03/s21-s22: finer shares of the largest tiles against the
+           per-workgroup set-up and flush) */
+        const int rounds = mode == kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 8);
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
