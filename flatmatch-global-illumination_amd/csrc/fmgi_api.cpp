@@ -205,6 +205,34 @@ FilterBuild build_filter(const fmgi_rect *walls, int nw, const fmgi_rect *srcs, 
     return fb;
 }
 
+/* ScanHybrid's wall filter image (FilterPairHalf): for the x and y axes, groups g of records 2g, 2g + 1 of
+   each class, in the class order of the filter image (rect order), +a class half first; G[a] groups */
+std::vector<FilterPairHalf> build_filter_pairs(const FilterBuild &fb, int G[2]) {
+    std::vector<FilterPairHalf> img;
+    for (int a = 0; a < 2; a++) {
+        G[a] = (fb.J[a] + 1) / 2;
+        for (int g = 0; g < G[a]; g++)
+            for (int c = 0; c < 2; c++) {
+                FilterPairHalf h;
+                for (int k = 0; k < 2; k++) {
+                    const size_t j = (size_t)(2 * g + k);
+                    const bool ok = j < fb.cls[a][c].size();
+                    FilterRec r;
+                    memset(&r, 0, sizeof r);
+                    if (ok) r = fb.cls[a][c][j];
+                    h.plane[k] = ok ? r.plane : 0.0f;
+                    h.cu[k] = ok ? r.cu : 0.0f;
+                    h.hwu[k] = ok ? r.hwu : -1.0f; /* |x| <= -1 never holds: never a candidate */
+                    h.cv[k] = ok ? r.cv : 0.0f;
+                    h.hwv[k] = ok ? r.hwv : -1.0f;
+                    h.idx[k] = ok ? r.idx : -1;
+                }
+                img.push_back(h);
+            }
+    }
+    return img;
+}
+
 template <class T>
 hipError_t upload(T **dst, const std::vector<T> &v) {
     hipError_t e = hipMalloc(dst, v.size() * sizeof(T));
@@ -589,6 +617,8 @@ struct fmgi_context {
     PlanBuild h_plan; /* ScanHybrid's floor plan of the walls (fmgi_plan_copy); h_plan.ok: built */
     std::vector<FilterRec> h_fimg; /* the filter image (fmgi_filter_copy) */
     int plan_off = -1; /* its byte offset in the hybrid image */
+    int pair_off = -1; /* byte offset of the hybrid image's wall pairs (FilterPairHalf groups) */
+    int pG[2] = {0, 0}; /* their groups per axis */
     int auto_kernel = FMGI_KERNEL_FAST;
     /* optional device timing (fmgi_set_timing) */
     bool timing = false;
@@ -975,7 +1005,11 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->h_plan = build_plan(fb, c->h_srcs.data(), (int)c->h_srcs.size());
     const std::vector<char> plan_blob = c->h_plan.ok ? c->h_plan.blob() : std::vector<char>();
     c->plan_off = c->h_plan.ok ? c->fimg_bytes + c->gimg_bytes : -1;
-    c->himg_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
+    const std::vector<FilterPairHalf> pairs_img = build_filter_pairs(fb, c->pG);
+    c->pair_off = (c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size() + 15) & ~15;
+    c->himg_bytes = c->pair_off + (int)(pairs_img.size() * sizeof(FilterPairHalf));
+    if (const char *pe = getenv("FMGI_PAIRS")) /* experiments: 0 = no pair image (FMGI_FILTER_PK=0 builds) */
+        if (atoi(pe) == 0) c->himg_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
     {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
@@ -1040,6 +1074,8 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
         memcpy(both.data(), fb.img.data(), (size_t)c->fimg_bytes);
         memcpy(both.data() + c->fimg_bytes, gb.img.data(), (size_t)c->gimg_bytes);
         if (!plan_blob.empty()) memcpy(both.data() + c->plan_off, plan_blob.data(), plan_blob.size());
+        if (c->pair_off + pairs_img.size() * sizeof(FilterPairHalf) <= both.size())
+            memcpy(both.data() + c->pair_off, pairs_img.data(), pairs_img.size() * sizeof(FilterPairHalf));
         hipFree(c->d_himg);
         c->d_himg = nullptr;
         HIPCHK(upload(&c->d_himg, both));
@@ -1367,6 +1403,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.gridx = c->d_gidx;
         a.grid_code_or = 0x40000000;
         a.plan_off = c->plan_off;
+        a.pair_off = c->pair_off;
+        a.pG[0] = c->pG[0];
+        a.pG[1] = c->pG[1];
     } else {
         a.fimg = c->d_fimg;
         a.fimg_bytes = c->fimg_bytes;

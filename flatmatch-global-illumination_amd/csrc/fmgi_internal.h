@@ -22,6 +22,16 @@ struct FilterRec {
 };
 static_assert(sizeof(FilterRec) == 32, "FilterRec must be 32 B");
 
+/* ScanHybrid's wall filter, two records per group (FilterPairs, 96 B): for each class c of the axis (+a
+   class first, then -a), records 2g and 2g + 1 of the class as field pairs, so each pair loads into a
+   64-bit register pair for packed fp32 ops: {plane0, plane1, cu0, cu1}, {hwu0, hwu1, cv0, cv1},
+   {hwv0, hwv1, idx0, idx1} (idx = rect index; a missing record is a never-valid sentinel, hwu = hwv = -1). */
+struct FilterPairHalf {
+    float plane[2], cu[2], hwu[2], cv[2], hwv[2];
+    int32_t idx[2];
+};
+static_assert(sizeof(FilterPairHalf) == 48, "FilterPairHalf must be 48 B");
+
 /* One plane of the grid kernel (ScanGrid): all axis-aligned rects of one class (axis a, normal sign)
    that lie in the plane x_a = plane, bucketed by a nu x nv grid over the plane's (u, v) bounding box of
    their margin-grown extents. Cell (iu, iv) = cells[cell_off + iv*nu + iu] = {first record, count}. */
@@ -83,6 +93,8 @@ struct BakeArgs {
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
     int plan_off;         /* ScanHybridPlan: byte offset of the floor plan in the image (-1: none)      */
+    int pair_off;         /* ScanHybrid: byte offset of the wall-pair image (FilterPairs) in the image  */
+    int pG[2];            /* ScanHybrid: FilterPairs groups per axis (x, y)                            */
     const uint32_t *fetch_tab;    /* fetch_nseg > 0: [f_begin, item_begin] pairs, f_begin ascending from 0:
                                      fetch f maps into the segment holding it (sums are order-free) */
     int fetch_nseg;

@@ -261,6 +261,54 @@ __device__ __forceinline__ void filter_axis(const char *img, int J, int sub, int
     }
 }
 
+/*
+ * ScanHybrid's wall filter: filter_axis over the pair image (FilterPairHalf, fmgi_internal.h), two records
+ * per iteration in packed fp32. A group holds records 2g and 2g + 1 of a class as field pairs, so each
+ * pair is a 64-bit register pair straight from ds_read_b128, and fac', the two hit coordinates and their
+ * offsets from the records' centres run as v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32: two fp32 ops per
+ * lane per issue slot (the f32 VALU peak on gfx950 is v_pk_fma_f32's, MI355X_MICROARCH.md). Each element
+ * is the same IEEE op on the same operands as filter_axis's, so every key and candidate test is
+ * filter_axis's bit for bit; the compares and the (L1, L2, code1) update stay per record, in record
+ * order. code1 receives the record's rect index itself (loaded with the fields), not a position.
+ */
+typedef float pkf2 __attribute__((ext_vector_type(2)));
+#ifndef FMGI_FILTER_PK
+#define FMGI_FILTER_PK 1
+#endif
+
+__device__ __forceinline__ void pair_rec(float f, float uu, float vv, float hu, float hv, int idx, float &L1,
+                                         float &L2, int &code1) {
+    const int ok = (int)(f >= 0.0f) & (int)(fabsf(uu) <= hu) & (int)(fabsf(vv) <= hv);
+    const float key = ok ? f : INFINITY;
+    const bool lt = key < L1;
+    L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+    code1 = lt ? idx : code1;
+    L1 = lt ? key : L1;
+}
+
+template <int A>
+__device__ __forceinline__ void filter_pairs(const char *img, int G, f3 s, f3 d, float &L1, float &L2,
+                                             int &code1) {
+    constexpr int U = (A == 0) ? 1 : 0;
+    constexpr int V = (A == 2) ? 1 : 2;
+    const float sa = comp<A>(s), da = comp<A>(d);
+    const float rd = __builtin_amdgcn_rcpf(da);
+    const pkf2 sa2 = {sa, sa}, rd2 = {rd, rd};
+    const pkf2 su2 = {comp<U>(s), comp<U>(s)}, sv2 = {comp<V>(s), comp<V>(s)};
+    const pkf2 du2 = {comp<U>(d), comp<U>(d)}, dv2 = {comp<V>(d), comp<V>(d)};
+    const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
+#pragma unroll 2
+    for (int g = 0; g < G; g++) {
+        const float4 q0 = p[6 * g], q1 = p[6 * g + 1], q2 = p[6 * g + 2];
+        const pkf2 pl = {q0.x, q0.y}, cu = {q0.z, q0.w}, cv = {q1.z, q1.w};
+        const pkf2 f = (pl - sa2) * rd2;
+        const pkf2 uu = __builtin_elementwise_fma(du2, f, su2) - cu;
+        const pkf2 vv = __builtin_elementwise_fma(dv2, f, sv2) - cv;
+        pair_rec(f.x, uu.x, vv.x, q1.x, q2.x, __float_as_int(q2.z), L1, L2, code1);
+        pair_rec(f.y, uu.y, vv.y, q1.y, q2.y, __float_as_int(q2.w), L1, L2, code1);
+    }
+}
+
 /* merges the phase-1 results (L1, L2, code1) of the coop lanes of a group (butterfly over lane ids):
    L1 = the minimum key, L2 = the second smallest of all keys, code1 = the winner (the smaller code on
    equal keys, so every lane of the group ends with the same values; equal keys fail the separation
@@ -799,8 +847,14 @@ struct ScanHybridT {
         if (Plan) { /* the walls the ray's floor-plan cells list, nearest cells first, after the floors */
             plan_walls(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
+#if FMGI_FILTER_PK
+            /* the walls: the pair image, two records per packed iteration; codes are rect indices */
+            filter_pairs<0>(lds + a.pair_off, a.pG[0], src, dir, L1, L2, code1);
+            filter_pairs<1>(lds + a.pair_off + 96 * a.pG[0], a.pG[1], src, dir, L1, L2, code1);
+#else       /* experiments (FMGI_FILTER_PK=0 builds): one record per iteration over the filter image */
             filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
             filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
+#endif
             ntest += (unsigned)(a.fJ[0] + a.fJ[1]);
         }
         cptr<int32_t> G = (cptr<int32_t>)a.general;
@@ -809,7 +863,7 @@ struct ScanHybridT {
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
             L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
-            code1 = lt ? ((3 << 16) | g) : code1;
+            code1 = lt ? (0x20000000 | g) : code1;
             L1 = lt ? key : L1;
         }
         st.tests += ntest + (uint32_t)a.ngeneral;
@@ -818,18 +872,20 @@ struct ScanHybridT {
             h.idx = -1;
             return;
         }
+        /* codes: grid records idx | 0x40000000, general rects g | 0x20000000, the pair filter's walls their
+           rect index; the floor plan's walls (A << 16) | position in the filter image */
         int idx;
         if (code1 & 0x40000000) {
             idx = code1 & 0x3FFFFFFF;
+        } else if (code1 & 0x20000000) {
+            idx = ((gptr<int32_t>)a.general)[code1 & 0x1FFFFFFF];
+        } else if (!Plan && FMGI_FILTER_PK) {
+            idx = code1;
         } else {
             const int A = code1 >> 16, j = code1 & 0xFFFF;
-            if (A == 3) {
-                idx = ((gptr<int32_t>)a.general)[j];
-            } else {
-                const float dA = A == 0 ? dir.x : dir.y;
-                const int off = A == 0 ? 0 : 64 * a.fJ[0];
-                idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
-            }
+            const float dA = A == 0 ? dir.x : dir.y;
+            const int off = A == 0 ? 0 : 64 * a.fJ[0];
+            idx = *(const int32_t *)(lds + off + 64 * j + (dA < 0.0f ? 0 : 32) + 20);
         }
         const float f = exact_hit(a, lds, idx, src, dir, h);
         if (!(f < 0) && L2 > f * 1.000244140625f) { /* ScanFast's separation test */
