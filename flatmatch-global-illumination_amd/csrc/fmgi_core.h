@@ -189,7 +189,11 @@ FMGI_HD int tile_uv(float dx, float dy, float wl, float hl, float iwl, float ihl
     int ty = trunc_div_inv(dy * (float)H, hl, ihl);
     tx = tx < 0 ? 0 : (tx > W - 1 ? W - 1 : tx);
     ty = ty < 0 ? 0 : (ty > H - 1 ? H - 1 : ty);
+#if defined(__HIP_DEVICE_COMPILE__)
+    return (int)__umul24((uint32_t)ty, (uint32_t)W) + tx; /* 0 <= ty < H, W < 2^24: not the quarter-rate v_mul_lo_u32 */
+#else
     return ty * W + tx;
+#endif
 }
 
 /* Warm-up skip-ahead (photonmap.cl:272-275): `r = rand()*40; for (i=0; i<r; i++) rand();` draws

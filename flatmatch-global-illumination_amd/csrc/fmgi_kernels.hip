@@ -128,8 +128,9 @@ __device__ __forceinline__ float exact_hit_rec(const R &r, int idx, f3 src, f3 d
    spaces (a pointer that may be either compiles to flat loads, which wait on both counters) */
 __device__ __forceinline__ float exact_hit(const BakeArgs &a, const char *lds, int idx, f3 src, f3 dir, HitRec &h) {
     if (uni(a.rects_off) >= 0)
-        return exact_hit_rec(((const __attribute__((address_space(3))) RectLds *)(
-                                 (const __attribute__((address_space(3))) char *)lds + a.rects_off))[idx],
+        return exact_hit_rec(*(const __attribute__((address_space(3))) RectLds *)(
+                                 (const __attribute__((address_space(3))) char *)lds + a.rects_off +
+                                 __umul24((uint32_t)idx, (uint32_t)sizeof(RectLds))), /* not the quarter-rate v_mul_lo_u32 */
                              idx, src, dir, h);
     return exact_hit_rec(((gptr<RectDev>)a.rects)[idx], idx, src, dir, h);
 }
