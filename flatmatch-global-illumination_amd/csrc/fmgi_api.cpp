@@ -616,6 +616,7 @@ struct fmgi_context {
     GridBuild h_grid; /* host copy (fmgi_grid_copy) */
     PlanBuild h_plan; /* ScanHybrid's floor plan of the walls (fmgi_plan_copy); h_plan.ok: built */
     std::vector<FilterRec> h_fimg; /* the filter image (fmgi_filter_copy) */
+    std::vector<FilterPairHalf> h_pairs; /* the hybrid scan's wall-pair image (fmgi_pairs_copy) */
     int plan_off = -1; /* its byte offset in the hybrid image */
     int pair_off = -1; /* byte offset of the hybrid image's wall pairs (FilterPairHalf groups) */
     int pG[2] = {0, 0}; /* their groups per axis */
@@ -1006,6 +1007,7 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     const std::vector<char> plan_blob = c->h_plan.ok ? c->h_plan.blob() : std::vector<char>();
     c->plan_off = c->h_plan.ok ? c->fimg_bytes + c->gimg_bytes : -1;
     const std::vector<FilterPairHalf> pairs_img = build_filter_pairs(fb, c->pG);
+    c->h_pairs = pairs_img;
     c->pair_off = (c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size() + 15) & ~15;
     c->himg_bytes = c->pair_off + (int)(pairs_img.size() * sizeof(FilterPairHalf));
     if (const char *pe = getenv("FMGI_PAIRS")) /* experiments: 0 = no pair image (FMGI_FILTER_PK=0 builds) */
@@ -1750,6 +1752,17 @@ FMGI_API int fmgi_grid_sizes(const fmgi_context *c, int32_t sizes[5]) {
     for (int a = 0; a < 3; a++) sizes[a] = c->h_grid.J[a];
     sizes[3] = (int32_t)c->h_grid.cells.size();
     sizes[4] = (int32_t)c->h_grid.idx.size();
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_pairs_copy(const fmgi_context *c, void *img, int32_t *bytes, int32_t groups[2]) {
+    if (!c || !bytes || !groups) return set_err(FMGI_ERR_ARG, "fmgi_pairs_copy: bad arguments");
+    const int32_t n = (int32_t)(c->h_pairs.size() * sizeof(FilterPairHalf));
+    if (img && *bytes < n) return set_err(FMGI_ERR_ARG, "fmgi_pairs_copy: buffer too small");
+    if (img && n) memcpy(img, c->h_pairs.data(), (size_t)n);
+    *bytes = n;
+    groups[0] = c->pG[0];
+    groups[1] = c->pG[1];
     return FMGI_OK;
 }
 

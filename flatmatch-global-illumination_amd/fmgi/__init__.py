@@ -233,6 +233,18 @@ class Context:
         recs = img.reshape(-1, 8)
         return {"J": [int(x) for x in J], "recs": recs, "idx": recs[:, 5].view(np.int32).copy()}
 
+    def pair_image(self) -> dict:
+        """The hybrid scan's wall-pair image (include/flatmatch_gi.h fmgi_pairs_copy): halves [n, 12] as
+        float32 (the two rect indices in columns 10, 11 as int32 bits), two halves (+a, -a) per group, and the
+        groups per axis (x, y)."""
+        n = C.c_int32(0)
+        G = np.zeros(2, np.int32)
+        check(self.lib.fmgi_pairs_copy(self.h, None, C.byref(n), _ptr(G)), "fmgi_pairs_copy")
+        img = np.zeros(n.value // 4, np.float32)
+        check(self.lib.fmgi_pairs_copy(self.h, _ptr(img), C.byref(n), _ptr(G)), "fmgi_pairs_copy")
+        halves = img.reshape(-1, 12)
+        return {"G": [int(x) for x in G], "halves": halves, "idx": halves[:, 10:12].view(np.int32).copy()}
+
     def device_sincosf(self, x: np.ndarray, library: bool = False):
         """The samplers' sin/cos on the device (the restatement), or with library=True the device
         library's sinf/cosf that it restates."""

@@ -44,6 +44,7 @@ EXPORTS = (
     "fmgi_grid_copy",
     "fmgi_plan_copy",
     "fmgi_filter_copy",
+    "fmgi_pairs_copy",
     "fmgi_get_stage_cycles",
     "fmgi_auto_kernel",
     "fmgi_set_timing",
@@ -210,6 +211,7 @@ def load() -> C.CDLL:
         "fmgi_grid_copy": (C.c_int, [vp, vp, vp, vp, vp]),
         "fmgi_plan_copy": (C.c_int, [vp, vp, vp]),
         "fmgi_filter_copy": (C.c_int, [vp, vp, vp, vp]),
+        "fmgi_pairs_copy": (C.c_int, [vp, vp, vp, vp]),
         "getGlobalIlluminationCl": (C.c_int, [C.POINTER(Geometry), C.c_int, vp]),
         "performGlobalIlluminationCl": (None, [C.POINTER(Geometry), C.c_int]),
     }

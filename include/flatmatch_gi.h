@@ -295,6 +295,11 @@ int fmgi_plan_copy(const fmgi_context *ctx, void *blob, int32_t *bytes);
    {float plane, cu, hwu, cv, hwv; int32 rect index (-1: padding); pad[2]} (32 B; extents grown by the
    filter margin). Pair j holds record j of each class, rect order. */
 int fmgi_filter_copy(const fmgi_context *ctx, void *img, int32_t *bytes, int32_t pairs[3]);
+/* FMGI_KERNEL_HYBRID's wall-pair image (built by fmgi_set_scene; host-only contexts too): for the x and then
+   the y axis, groups[a] groups of two 48-B halves (the +a class, then the -a class), each half
+   {float plane[2], cu[2], hwu[2], cv[2], hwv[2]; int32 rect index[2]} = records 2g and 2g + 1 of its class as
+   the filter image holds them (a missing record: hwu = hwv = -1, index -1). Same size protocol. */
+int fmgi_pairs_copy(const fmgi_context *ctx, void *img, int32_t *bytes, int32_t groups[2]);
 
 /* Host helpers exported for tests (no device needed). */
 void fmgi_host_sincosf(const float *x, float *s, float *c, int64_t n);
