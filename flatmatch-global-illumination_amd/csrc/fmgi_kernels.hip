@@ -844,14 +844,15 @@ struct ScanHybridT {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         unsigned ntest = 0;
-        grid_axis<2>(a, lds + a.hyb_off, 128 * (a.gJ[0] + a.gJ[1]), a.gJ[2], src, dir, L1, L2, code1, ntest);
+        grid_axis<2>(a, lds + uni(a.hyb_off), 128 * (uni(a.gJ[0]) + uni(a.gJ[1])), uni(a.gJ[2]), src, dir, L1, L2,
+                     code1, ntest);
         if (Plan) { /* the walls the ray's floor-plan cells list, nearest cells first, after the floors */
             plan_walls(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
 #if FMGI_FILTER_PK
             /* the walls: the pair image, two records per packed iteration; codes are rect indices */
-            filter_pairs<0>(lds + a.pair_off, a.pG[0], src, dir, L1, L2, code1);
-            filter_pairs<1>(lds + a.pair_off + 96 * a.pG[0], a.pG[1], src, dir, L1, L2, code1);
+            filter_pairs<0>(lds + uni(a.pair_off), uni(a.pG[0]), src, dir, L1, L2, code1);
+            filter_pairs<1>(lds + uni(a.pair_off) + 96 * uni(a.pG[0]), uni(a.pG[1]), src, dir, L1, L2, code1);
 #else       /* experiments (FMGI_FILTER_PK=0 builds): one record per iteration over the filter image */
             filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
             filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
