@@ -1010,8 +1010,8 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->h_pairs = pairs_img;
     c->pair_off = (c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size() + 15) & ~15;
     c->himg_bytes = c->pair_off + (int)(pairs_img.size() * sizeof(FilterPairHalf));
-    if (const char *pe = getenv("FMGI_PAIRS")) /* experiments: 0 = no pair image (FMGI_FILTER_PK=0 builds) */
-        if (atoi(pe) == 0) c->himg_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
+    if (const char *pe = getenv("FMGI_PAIRS")) /* experiments: 0 = no pair image (honoured by FMGI_FILTER_PK=0 builds) */
+        if (atoi(pe) == 0 && !fmgi_kernels_filter_pk()) c->himg_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
     {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];

@@ -186,6 +186,7 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off);
+int fmgi_kernels_filter_pk(); /* the kernels' FMGI_FILTER_PK (whether the hybrid scan reads the pair image) */
 hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long *colfx, unsigned long long *lm,
                                      int n, hipStream_t s);
 hipError_t fmgi_launch_add_u64(unsigned long long *dst, const unsigned long long *src, int64_t n, hipStream_t s);

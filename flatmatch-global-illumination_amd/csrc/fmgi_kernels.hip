@@ -1790,6 +1790,9 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
 } // namespace
 
 /* dynamic LDS of a bake launch: the scan image (fast / grid scans), then one ring per wave (AccStream) */
+/* 1 when this build's hybrid scan reads the wall-pair image (the default), 0 for FMGI_FILTER_PK=0 builds */
+int fmgi_kernels_filter_pk() { return FMGI_FILTER_PK; }
+
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
