@@ -893,7 +893,9 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         /* bucketed: ~36 rounds (box200, 46 tiles: fold 11.22 / 10.86 / 10.92 / 11.19 / 12.70 ms at 96 / 200 /
            300 / 800 / 1600 groups, profiles/r03/s21-s22: finer shares of the largest tiles against the
            per-workgroup set-up and flush) */
-        const int rounds = mode == kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 8);
+        /* slice-sorted (lightmaps of more than 63 tiles): ~48 rounds (30-room layout, 358 tiles: fold 7.49 /
+           7.31 / 6.34 / 5.97 ms at 8 / 4 / 16 / 32 groups per tile, profiles/r03/s33) */
+        const int rounds = mode == kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 48);
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
@@ -904,6 +906,9 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
             if (mode == kStreamBuckets) /* at least one 4-KB block per wave of every workgroup */
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
                                                     std::max<uint64_t>(8, (cap / FMGI_BUCKET_BLOCK) / ((uint64_t)P * 16)));
+            if (mode == kStreamSliced) /* at least one big slice's worth of codes per workgroup and tile */
+                sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
+                                                    std::max<uint64_t>(8, cap / ((uint64_t)P * FMGI_STREAM_SLICE_BIG)));
         }
         const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
