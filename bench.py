@@ -39,17 +39,20 @@ CONFIGS = {
 }
 METRIC = "photons/sec + achieved HBM GB/s (% of peak), 200-rect scene, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0     # MI355X_MICROARCH.md: 8.0 TB/s spec
+VALU_PEAK_TFLOPS = 157.3  # MI355X_MICROARCH.md: FP32 vector peak (spec) = 0.5 wave64 v_fma_f32 per SIMD-cycle at 2.4 GHz
 
 
 def valu_peak():
-    """Measured wave64 VALU issue ceiling of one MI355X per SIMD-cycle at the measured in-kernel clock
-    (tools/valu_peak.hip, >= 50 ms launches -> profiles/valu_peak.json), by resident waves per SIMD."""
+    """Measured wave64 v_fma_f32 issue ceiling of one MI355X SIMD per shader cycle, by resident waves per
+    SIMD (tools/valu_peak.hip: per-SIMD s_memtime stamps with HW_ID placement, >= 50 ms launches ->
+    profiles/valu_peak.json), its saturated value (8 waves) and the spec's 0.5."""
     p = os.path.join(REPO, "profiles", "valu_peak.json")
     try:
         d = json.load(open(p))
-        return {int(k): float(v) for k, v in d["f32_per_simd_per_clk_by_waves"].items()}, d.get("source", p)
+        by = {int(k): float(v) for k, v in d["f32_per_simd_per_clk_by_waves"].items()}
+        return by, d.get("source", p), max(by.values()), d.get("spec_fma_per_simd_cycle", 0.5)
     except (OSError, ValueError, KeyError):
-        return None, None
+        return None, None, None, 0.5
 
 
 def load_scene(name):
@@ -140,6 +143,48 @@ def cpu_baseline_reference(sc, target_s=10.0, procs=1):
     }
 
 
+def cpu_baseline_radiosity(target_s=10.0, procs=1):
+    """The reference's radiosityNative path (performRadiosityNative, radiosityNative.c:92-268), built from
+    /root/reference by oracle/build_ref.sh into oracle/_ref/rad_ref, timed on this host on the tiny lit box
+    (box200 with 2-m tiles and a ceiling light: 830 wall texels, 8.3e6 form-factor rays, ~10 s on one core):
+    `procs` concurrent single-threaded processes (one per host thread), value = their rays / the slowest
+    one's time. A different algorithm and unit (form-factor rays, not photons): reported beside the photon
+    numbers as north_star asks, not comparable with them. None if the build is absent."""
+    import subprocess
+    import tempfile
+
+    from fmgi import scene as S
+
+    exe = os.path.join(REPO, "oracle", "_ref", "rad_ref")
+    if not os.path.exists(exe):
+        return None
+    sc = S.box_scene(200, tile_size=2.0, with_light=True)
+    rays = 10_000 * int(sum(int(w["lightmapSetup"][1]) * int(w["lightmapSetup"][2]) for w in sc.walls))
+    with tempfile.TemporaryDirectory() as d:
+        g = os.path.join(d, "geometry.bin")
+        S.save_geometry(sc, g)
+        t0 = time.perf_counter()
+        ps = [subprocess.Popen([exe, g, os.path.join(d, f"tex{k}.bin"), "1"], stdout=subprocess.DEVNULL)
+              for k in range(procs)]
+        ends = []
+        for p in ps:
+            p.wait(timeout=max(300.0, 30 * target_s))
+            ends.append(time.perf_counter() - t0)
+        if any(p.returncode for p in ps):
+            raise RuntimeError("rad_ref failed")
+    secs = max(ends)
+    return {
+        "value": procs * rays / secs,
+        "unit": "form-factor rays/s",
+        "cores": procs,
+        "kind": "reference",
+        "comparable": False,
+        "sample": f"the reference's performRadiosityNative (oracle/_ref/rad_ref, built from /root/reference): "
+                  f"{procs} concurrent process(es) x {rays} rays (box200, 2-m tiles, ceiling light; 7 bounces), "
+                  f"slowest {secs:.1f} s. Not photon-comparable: a different algorithm and unit",
+    }
+
+
 def pmc_traffic(config_name):
     """HBM bytes per bake launch from the committed rocprofv3 PMC summary (profiles/), if present."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
@@ -182,7 +227,7 @@ def issue_block(rec, ks, per_launch_scans, cus):
     insts = {k: per.get(f"SQ_INSTS_{k}", 0.0) for k in ("VALU", "SALU", "SMEM", "BRANCH", "VMEM", "LDS")}
     total = sum(insts.values())
     waves_per_simd = per["SQ_WAVES"] / (4.0 * cus)
-    peaks, peak_src = valu_peak()
+    peaks, peak_src, vsat, vspec = valu_peak()
     vpeak = None
     if peaks:
         w = max(1, int(round(waves_per_simd)))
@@ -201,6 +246,10 @@ def issue_block(rec, ks, per_launch_scans, cus):
         "insts_per_simd_cycle": total / simd_cycles,
         "valu_peak_per_simd_cycle": vpeak,
         "valu_frac_of_peak": vpc / vpeak if vpeak else None,
+        "valu_saturated_per_simd_cycle": vsat,
+        "valu_frac_of_saturated": vpc / vsat if vsat else None,
+        "valu_spec_per_simd_cycle": vspec,
+        "valu_frac_of_spec": vpc / vspec,
         "wave_cycles": {"issuing": per["SQ_ACTIVE_INST_ANY"] / wc, "issue_stalled": per["SQ_WAIT_INST_ANY"] / wc,
                         "waiting": per["SQ_WAIT_ANY"] / wc},
         "insts_per_launch": insts,
@@ -312,7 +361,7 @@ def main():
     tex_in = torch.zeros((sc.num_texels, 4), dtype=torch.float32, device=dev)
     tex_out = torch.empty_like(tex_in)
 
-    k_ms = []
+    k_ms, r_ms = [], []
 
     def step(timed):
         lm.zero_()
@@ -325,6 +374,10 @@ def main():
             k_ms.append((s_ev, e_ev))
         if world > 1:
             parallel.reduce_lightmap(lm, dst=0)  # RCCL over xGMI
+            if timed:  # the reduce as this rank's stream sees it: from the bake's end to the reduce's end
+                r_ev = torch.cuda.Event(enable_timing=True)
+                r_ev.record(stream)
+                r_ms.append((e_ev, r_ev))
         if rank == 0:
             ctx.finalize(lm.data_ptr(), tex_in.data_ptr(), tex_out.data_ptr(), sptr)
 
@@ -351,6 +404,21 @@ def main():
     tim = ctx.timing()
     bake_launch_ms = tim["bake_ms"] / max(tim["bake_launches"], 1)  # the dominant kernel, per launch
     bake_launches = tim["bake_launches"]
+    # every rank's photon counter must cover exactly its shard (no work skipped or repeated)
+    shard_photons = 100 * (e - b) * args.steps
+    if int(st["photons"]) != shard_photons:
+        raise SystemExit(f"rank {rank}: photon counter {st['photons']} != its shard's {shard_photons}")
+    if world > 1:  # per-rank breakdown, gathered to every rank (diagnoses the driver's multi-GPU runs)
+        row = [float(rank), float(device_index), float(b), float(e), float(st["photons"]), bake_launch_ms,
+               float(bake_launches) / args.steps, tim["fold_ms"] / args.steps, span_ms,
+               float(np.mean([s0.elapsed_time(s1) for s0, s1 in r_ms])), elapsed * 1e3 / args.steps]
+        keys = ("rank", "device", "item_begin", "item_end", "photons", "k_bake_ms_per_launch", "k_bake_launches_per_step",
+                "fold_ms_per_step", "bake_path_ms_per_step", "reduce_ms_per_step", "wall_ms_per_step")
+        rows = parallel.gather_rows(row, dev)
+        dist_info["per_rank"] = [{k: (int(v) if k in ("rank", "device", "item_begin", "item_end", "photons") else v)
+                                  for k, v in zip(keys, r)} for r in rows]
+        dist_info["reduce_ms_per_step_max"] = max(r[9] for r in rows)
+        dist_info["k_bake_ms_per_launch_spread"] = [min(r[5] for r in rows), max(r[5] for r in rows)]
 
     vals = torch.tensor([elapsed, st["scans"], st["deposits"], st["photons"]], dtype=torch.float64, device=dev)
     if world > 1:
@@ -386,6 +454,27 @@ def main():
         issue = issue_block(rec, ks, per_launch_scans, torch.cuda.get_device_properties(dev).multi_processor_count) \
             if rec else None
         bound, binding = binding_of(issue, atomic_rate)
+        # SURVEY.md §8d FLOP roofline of the same launches: F = 40 x T + 150 x S per photon (40 = one
+        # branch-free intersects(), 150 = sampling, tile index and colour per bounce), S = scans per photon,
+        # T = rect tests per photon -- the tests this bake evaluates (its scans test a few records each), and
+        # the reference's linear scan (every rect per scan, T = rects x S) as the algorithmic equivalent
+        ph_launch = st["photons"] / bake_launches
+        s_bar = per_launch_scans / ph_launch
+        t_eval = st["tests"] / bake_launches / ph_launch
+        f_eval = 40.0 * t_eval + 150.0 * s_bar
+        f_lin = 40.0 * len(sc.walls) * s_bar + 150.0 * s_bar
+        flops = {
+            "bound_unit": "TFLOP/s", "peak": VALU_PEAK_TFLOPS,
+            "scans_per_photon": s_bar, "rect_tests_per_photon": t_eval,
+            "flops_per_photon": f_eval,
+            "achieved": f_eval * ph_launch / ks / 1e12,
+            "frac": f_eval * ph_launch / ks / 1e12 / VALU_PEAK_TFLOPS,
+            "linear_scan_flops_per_photon": f_lin,
+            "linear_scan_equivalent": f_lin * ph_launch / ks / 1e12,
+            "linear_scan_equivalent_frac": f_lin * ph_launch / ks / 1e12 / VALU_PEAK_TFLOPS,
+            "note": "achieved/frac count the rect tests the bake evaluates; linear_scan_* the reference's "
+                    "rects x scans (SURVEY.md §8d), which the acceleration structure does not execute",
+        }
         out = {
             "metric": METRIC,
             "value": value,
@@ -439,6 +528,7 @@ def main():
                         "note": "rect tests = phase-1 record tests + exact tests the scans evaluated "
                                 "(the reference's linear scan would do rects x scans)"},
             },
+            "flops": flops,
             "per_photon": {
                 "scans": scans / photons_done,
                 "deposits": deposits / photons_done,
@@ -471,6 +561,9 @@ def main():
             ref = cpu_baseline_reference(sc, args.cpu_seconds, procs=cpu_threads())
             if ref is not None:
                 out["cpu_baseline_reference_native"] = ref
+            rad = cpu_baseline_radiosity(args.cpu_seconds, procs=cpu_threads())
+            if rad is not None:  # north_star: radiosityNative.c timed on the host cores in the same run
+                out["cpu_baseline_radiosity"] = rad
         print(json.dumps(out), flush=True)
     ctx.close()
     if world > 1:

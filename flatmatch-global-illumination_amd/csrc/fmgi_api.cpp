@@ -608,8 +608,12 @@ struct fmgi_context {
     int gimg_bytes = 0;
     int gJ[3] = {0, 0, 0};
     GridCell *d_gcells = nullptr;
-    char *d_himg = nullptr;       /* ScanHybrid: the filter image followed by the grid's plane image */
+    char *d_himg = nullptr;       /* ScanHybrid (default instance): the grid's plane image, then the wall pairs */
     int himg_bytes = 0;
+    char *d_himg_full = nullptr;  /* ... the floor-plan walk and FMGI_FILTER_PK=0 builds: filter image | plane
+                                     image | floor plan | wall pairs */
+    int himg_full_bytes = 0;
+    int pair_off_full = -1;
     float *d_grecs = nullptr;
     int32_t *d_gidx = nullptr;
     int grid_cells = 0, grid_entries = 0;
@@ -617,8 +621,8 @@ struct fmgi_context {
     PlanBuild h_plan; /* ScanHybrid's floor plan of the walls (fmgi_plan_copy); h_plan.ok: built */
     std::vector<FilterRec> h_fimg; /* the filter image (fmgi_filter_copy) */
     std::vector<FilterPairHalf> h_pairs; /* the hybrid scan's wall-pair image (fmgi_pairs_copy) */
-    int plan_off = -1; /* its byte offset in the hybrid image */
-    int pair_off = -1; /* byte offset of the hybrid image's wall pairs (FilterPairHalf groups) */
+    int plan_off = -1; /* its byte offset in the full hybrid image */
+    int pair_off = -1; /* byte offset of the (default) hybrid image's wall pairs (FilterPairHalf groups) */
     int pG[2] = {0, 0}; /* their groups per axis */
     int auto_kernel = FMGI_KERNEL_FAST;
     /* optional device timing (fmgi_set_timing) */
@@ -725,6 +729,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_gimg);
     hipFree(c->d_gcells);
     hipFree(c->d_himg);
+    hipFree(c->d_himg_full);
     hipFree(c->d_blob);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
@@ -957,8 +962,16 @@ static const size_t kBakeLdsLimit = 65536;
 /* ... and with the limit raised (fmgi_launch_bake sets the kernel attribute): what staging may use */
 static const size_t kBakeLdsMax = 160 * 1024;
 
+/* whether a hybrid bake reads the full image (the floor-plan walk, FMGI_PLAN=1, or the one-record wall loop
+   of FMGI_FILTER_PK=0 builds) rather than the default one (plane image + wall pairs only) */
+static bool hybrid_full(const fmgi_context *c) {
+    const char *pe = getenv("FMGI_PLAN");
+    return !fmgi_kernels_filter_pk() || (c->plan_off >= 0 && pe && atoi(pe) == 1);
+}
+
 static int image_bytes(const fmgi_context *c, int kernel) {
-    return kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : (kernel == FMGI_KERNEL_HYBRID ? c->himg_bytes : c->fimg_bytes);
+    if (kernel == FMGI_KERNEL_HYBRID) return hybrid_full(c) ? c->himg_full_bytes : c->himg_bytes;
+    return kernel == FMGI_KERNEL_GRID ? c->gimg_bytes : c->fimg_bytes;
 }
 
 static bool kernel_fits(const fmgi_context *c, int kernel, int accum, int block) {
@@ -1013,10 +1026,14 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->plan_off = c->h_plan.ok ? c->fimg_bytes + c->gimg_bytes : -1;
     const std::vector<FilterPairHalf> pairs_img = build_filter_pairs(fb, c->pG);
     c->h_pairs = pairs_img;
-    c->pair_off = (c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size() + 15) & ~15;
-    c->himg_bytes = c->pair_off + (int)(pairs_img.size() * sizeof(FilterPairHalf));
+    const int pairs_bytes = (int)(pairs_img.size() * sizeof(FilterPairHalf));
+    c->pair_off_full = (c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size() + 15) & ~15;
+    c->himg_full_bytes = c->pair_off_full + pairs_bytes;
     if (const char *pe = getenv("FMGI_PAIRS")) /* experiments: 0 = no pair image (honoured by FMGI_FILTER_PK=0 builds) */
-        if (atoi(pe) == 0 && !fmgi_kernels_filter_pk()) c->himg_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
+        if (atoi(pe) == 0 && !fmgi_kernels_filter_pk()) c->himg_full_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
+    /* the default instance stages only what it reads: the plane image (a multiple of 64 B) and the pairs */
+    c->pair_off = c->gimg_bytes;
+    c->himg_bytes = c->pair_off + pairs_bytes;
     {   /* AUTO: phase-1 work per scan ~ 60 VALU per grid plane slot vs ~15 per filter pair (measured on
            the example layout and the synthetic boxes: GRID 1.3-11x faster on boxes, 0.6x on example) */
         const int slots = gb.J[0] + gb.J[1] + gb.J[2], pairs = fb.J[0] + fb.J[1] + fb.J[2];
@@ -1076,16 +1093,23 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->d_gidx = nullptr;
     HIPCHK(upload(&c->d_gimg, gb.img));
     HIPCHK(upload(&c->d_gcells, gb.cells));
-    {   /* ScanHybrid's image: the filter image (a multiple of 64 B), then the plane image, then the plan */
-        std::vector<char> both((size_t)c->himg_bytes);
+    {   /* ScanHybrid's full image: the filter image (a multiple of 64 B), the plane image, the plan, the pairs */
+        std::vector<char> both((size_t)c->himg_full_bytes);
         memcpy(both.data(), fb.img.data(), (size_t)c->fimg_bytes);
         memcpy(both.data() + c->fimg_bytes, gb.img.data(), (size_t)c->gimg_bytes);
         if (!plan_blob.empty()) memcpy(both.data() + c->plan_off, plan_blob.data(), plan_blob.size());
-        if (c->pair_off + pairs_img.size() * sizeof(FilterPairHalf) <= both.size())
-            memcpy(both.data() + c->pair_off, pairs_img.data(), pairs_img.size() * sizeof(FilterPairHalf));
+        if (c->pair_off_full + pairs_img.size() * sizeof(FilterPairHalf) <= both.size())
+            memcpy(both.data() + c->pair_off_full, pairs_img.data(), pairs_img.size() * sizeof(FilterPairHalf));
+        hipFree(c->d_himg_full);
+        c->d_himg_full = nullptr;
+        HIPCHK(upload(&c->d_himg_full, both));
+        /* ... and the default instance's: the plane image, then the pairs */
+        std::vector<char> img((size_t)c->himg_bytes);
+        memcpy(img.data(), gb.img.data(), (size_t)c->gimg_bytes);
+        memcpy(img.data() + c->pair_off, pairs_img.data(), pairs_img.size() * sizeof(FilterPairHalf));
         hipFree(c->d_himg);
         c->d_himg = nullptr;
-        HIPCHK(upload(&c->d_himg, both));
+        HIPCHK(upload(&c->d_himg, img));
     }
     HIPCHK(upload(&c->d_grecs, gb.recs));
     HIPCHK(upload(&c->d_gidx, gb.idx));
@@ -1398,9 +1422,10 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.grid_axes = grid_axes_scene(c) ? 1 : 0;
         a.grid_xy_separate = getenv("FMGI_GRID_SEPARATE") ? 1 : 0;
     } else if (kernel == FMGI_KERNEL_HYBRID) {
-        a.fimg = c->d_himg;
-        a.fimg_bytes = c->himg_bytes;
-        a.hyb_off = c->fimg_bytes;
+        const bool full = hybrid_full(c);
+        a.fimg = full ? c->d_himg_full : c->d_himg;
+        a.fimg_bytes = full ? c->himg_full_bytes : c->himg_bytes;
+        a.hyb_off = full ? c->fimg_bytes : 0;
         for (int k = 0; k < 3; k++) {
             a.fJ[k] = c->fJ[k];
             a.gJ[k] = c->gJ[k];
@@ -1409,8 +1434,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
         a.grid_code_or = 0x40000000;
-        a.plan_off = c->plan_off;
-        a.pair_off = c->pair_off;
+        a.plan_off = full ? c->plan_off : -1;
+        a.pair_off = full ? c->pair_off_full : c->pair_off;
         a.pG[0] = c->pG[0];
         a.pG[1] = c->pG[1];
     } else {
@@ -1420,8 +1445,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     }
     a.rects_off = a.srcs_off = -1;
     if (sp.rects_off >= 0 || sp.srcs_off >= 0) { /* the blob: image | RectDev table | SrcDev table */
-        const uint64_t key = (c->scene_gen << 8) | ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) |
-                             (sp.srcs_off >= 0 ? 1u : 0u);
+        const uint64_t key = (c->scene_gen << 8) | (kernel == FMGI_KERNEL_HYBRID && hybrid_full(c) ? 0x40u : 0u) |
+                             ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) | (sp.srcs_off >= 0 ? 1u : 0u);
         if (c->blob_key != key) {
             if (c->blob_cap < (size_t)sp.bytes) {
                 HIPCHK(hipStreamSynchronize(s)); /* no earlier bake may still stage the old blob */
@@ -2040,8 +2065,10 @@ static void enable_peer(int dev, int peer) {
 /*
  * RCCL for the drop-in's one-process multi-GPU reduce (ncclCommInitAll over the shard devices,
  * one ncclReduce of the int64 lightmaps to shard 0 over xGMI). librccl is opened on the first call that
- * needs it, so single-GPU callers of the library never load it; the communicators are cached with the
- * shards (fmgi_dropin_release destroys them).
+ * reduces through it, so single-GPU callers of the library never load it (releasing with no communicator
+ * does not open it either); the communicators are cached with the shards (fmgi_dropin_release destroys
+ * them). When librccl cannot be loaded or ncclCommInitAll fails and FMGI_REDUCE=rccl was not set, the call
+ * reduces by xGMI peer copies instead (the same integer sums, so the same bits).
  */
 struct RcclApi {
     void *h = nullptr;
@@ -2079,13 +2106,17 @@ static const RcclApi *rccl_api() {
 
 static std::vector<ncclComm_t> g_rccl_comms; /* one per shard, over the shard devices in shard order */
 static std::vector<int> g_rccl_devs;
+static bool g_rccl_last = false; /* whether the last drop-in call reduced through RCCL */
 
 static void rccl_release() {
-    const RcclApi *R = rccl_api();
-    if (R)
-        for (ncclComm_t cm : g_rccl_comms) (void)R->comm_destroy(cm);
+    if (!g_rccl_comms.empty()) { /* comms exist only once librccl was loaded: no dlopen otherwise */
+        const RcclApi *R = rccl_api();
+        if (R)
+            for (ncclComm_t cm : g_rccl_comms) (void)R->comm_destroy(cm);
+    }
     g_rccl_comms.clear();
     g_rccl_devs.clear();
+    g_rccl_last = false;
 }
 
 /* communicators over `devs` (distinct devices; rank k = shard k), created once per device list */
@@ -2102,11 +2133,13 @@ static int rccl_comms(const std::vector<int> &devs) {
     return FMGI_OK;
 }
 
-/* ranks of the cached communicator (ncclCommCount of rank 0's), 0 if none */
+/* ranks of the communicator the last drop-in call reduced through (ncclCommCount of rank 0's), 0 if that
+   call did not reduce through RCCL */
 FMGI_API int fmgi_dropin_rccl_ranks(void) {
+    if (!g_rccl_last || g_rccl_comms.empty()) return 0;
     const RcclApi *R = rccl_api();
     int n = 0;
-    if (!R || g_rccl_comms.empty() || R->comm_count(g_rccl_comms[0], &n) != ncclSuccess) return 0;
+    if (!R || R->comm_count(g_rccl_comms[0], &n) != ncclSuccess) return 0;
     return n;
 }
 
@@ -2151,13 +2184,32 @@ FMGI_API int fmgi_dropin_reduce_order(int nshard, int32_t *dst, int32_t *src) {
  * reference's one device; at most 8). The reference launch schedule is built once (libc rand() consumed
  * exactly as the reference does, global_illumination_cl.c:251) and its flattened work items are split
  * into equal contiguous shards, one per GPU, prepared and launched concurrently (a host thread per
- * shard); each GPU accumulates its own exact int64 lightmap, and the shards are summed in a binary tree
- * over xGMI peer copies into shard 0 (integer sums: bit-identical for any GPU count). FMGI_SHARDS (tests)
- * splits into more shards than GPUs, round-robin, to exercise the reduction on a single device.
+ * shard); each GPU accumulates its own exact int64 lightmap, and the shards are summed into shard 0 by one
+ * RCCL reduce over the shard devices (default with one shard per device) or by a binary tree of xGMI peer
+ * copies (FMGI_REDUCE=peer, shards sharing a device, or RCCL unavailable); integer sums are bit-identical
+ * for any GPU count and either reduce. FMGI_SHARDS (tests) splits into more shards than GPUs, round-robin,
+ * to exercise the reduction on a single device.
  */
 static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int kernel,
                                  const std::vector<int32_t> &offs, uint64_t items, fmgi_vec3 *texels_out,
                                  bool verbose);
+
+/* photonMapLightSource's progress line before each launch, with the samples (work items) still to launch
+   for that source, and a newline after each source (global_illumination_cl.c:248-249, :267): the same
+   bytes the reference writes, printed once the launches are queued */
+static void print_launch_progress(const std::vector<LaunchDev> &launches) {
+    for (size_t i = 0; i < launches.size();) {
+        size_t j = i;
+        uint64_t left = 0;
+        while (j < launches.size() && launches[j].source == launches[i].source) left += launches[j++].count;
+        for (size_t k = i; k < j; k++) {
+            printf("\rphoton-mapping window with %d M samples   ", (int)(left * 100 / 1000000));
+            left -= launches[k].count;
+        }
+        printf("\n");
+        i = j;
+    }
+}
 
 static int bake_geometry(const fmgi_geometry *geo, int spa, fmgi_vec3 *texels_out, bool verbose) {
     if (!geo) return set_err(FMGI_ERR_ARG, "null geometry");
@@ -2299,12 +2351,12 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
     for (int k = 0; k < nshard; k++)
         if (rcs[(size_t)k] != FMGI_OK) return set_err(rcs[(size_t)k], "shard %d: %s", k, errs[(size_t)k].c_str());
     DropinShard &S0 = g_dropin[0];
-    if (verbose) {
+    if (verbose) { /* the reference's console output (global_illumination_cl.c:59, :248-249, :267) */
         hipDeviceProp_t prop;
         if (hipGetDeviceProperties(&prop, S0.ctx->device) != hipSuccess) prop.name[0] = 0;
-        printf("[INF] Selected device '%s' (x%d)\n\n", prop.name, ngpu);
-        printf("photon-mapping %d light sources with %llu M samples in %lld reference launches\n", S0.ctx->nsrcs,
-               (unsigned long long)(items * 100 / 1000000), (long long)S0.ctx->h_launches.size());
+        if (ngpu > 1) printf("[INF] Selected device '%s' (x%d)\n\n", prop.name, ngpu);
+        else printf("[INF] Selected device '%s'\n\n", prop.name);
+        print_launch_progress(S0.ctx->h_launches);
         fflush(stdout);
     }
     if (geo->numTexels <= 0) return FMGI_OK;
@@ -2318,10 +2370,20 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
         for (int j = 0; j < k; j++) distinct = distinct && sdev[(size_t)k] != sdev[(size_t)j];
     const bool force_rccl = r_env && !strcmp(r_env, "rccl"), force_peer = r_env && !strcmp(r_env, "peer");
     if (force_rccl && !distinct) return set_err(FMGI_ERR_ARG, "FMGI_REDUCE=rccl needs one shard per device");
-    const bool use_rccl = force_rccl || (nshard > 1 && distinct && !force_peer);
+    bool use_rccl = force_rccl || (nshard > 1 && distinct && !force_peer);
+    g_rccl_last = false;
     if (use_rccl) {
         int rc = rccl_comms(std::vector<int>(sdev.begin(), sdev.end()));
-        if (rc != FMGI_OK) return rc;
+        if (rc != FMGI_OK && force_rccl) return rc;
+        if (rc != FMGI_OK) { /* RCCL not loadable or its init failed: the peer-copy tree gives the same sums */
+            if (verbose) {
+                printf("[INF] RCCL unavailable (%s); shards reduced by xGMI peer copies\n", fmgi_last_error());
+                fflush(stdout);
+            }
+            use_rccl = false;
+        }
+    }
+    if (use_rccl) {
         const RcclApi *R = rccl_api();
         ncclResult_t r = R->group_start();
         for (int k = 0; k < nshard && r == ncclSuccess; k++) {
@@ -2333,6 +2395,7 @@ static int bake_geometry_devices(const fmgi_geometry *geo, int spa, int wg, int 
         const ncclResult_t r2 = R->group_end();
         if (r == ncclSuccess) r = r2;
         if (r != ncclSuccess) return set_err(FMGI_ERR_HIP, "ncclReduce of the shard lightmaps: %s", R->error_string(r));
+        g_rccl_last = true;
     }
     /* binary-tree reduction into shard 0 (fmgi_dropin_reduce_order), ordered by events across devices */
     std::vector<int32_t> rdst((size_t)nshard), rsrc((size_t)nshard);

@@ -40,6 +40,22 @@ def reduce_lightmap(lm, dst: int = 0, group=None):
     return lm
 
 
+def gather_rows(row, device=None, group=None):
+    """Every rank's row of floats (equal lengths), gathered to every rank in rank order: the per-rank
+    timing breakdown bench.py reports at N > 1. float64 so item offsets and photon counts stay exact."""
+    import torch
+    import torch.distributed as dist
+
+    t = torch.tensor([float(x) for x in row], dtype=torch.float64, device=device)
+    if not (dist.is_available() and dist.is_initialized()) or dist.get_world_size(group) == 1:
+        return [t.tolist()]
+    if t.is_cuda and _host_backend(group):
+        t = t.cpu()
+    out = [torch.empty_like(t) for _ in range(dist.get_world_size(group))]
+    dist.all_gather(out, t, group=group)
+    return [x.tolist() for x in out]
+
+
 def all_reduce(t, op, group=None):
     """dist.all_reduce, staging device tensors through host memory on gloo."""
     import torch.distributed as dist

@@ -27,8 +27,9 @@ def test_issue_block_from_committed_counters_is_bounded():
     scans = 8.0e9  # box200: scans per launch (bench per_photon.scans x photons)
     iss = b.issue_block(rec, kernel_s, scans, 256)
     assert iss is not None
-    for k in ("valu_frac_of_peak",):
+    for k in ("valu_frac_of_peak", "valu_frac_of_saturated", "valu_frac_of_spec"):
         assert 0 < iss[k] <= 1.05, (k, iss[k])
+    assert iss["valu_peak_per_simd_cycle"] <= iss["valu_saturated_per_simd_cycle"] <= iss["valu_spec_per_simd_cycle"]
     w = iss["wave_cycles"]
     assert abs(w["issuing"] + w["issue_stalled"] + w["waiting"] - 1.0) < 0.02, w
     for k, v in iss["vmem_path"].items():
@@ -48,3 +49,16 @@ def test_traffic_summary_is_committed():
     assert d["hbm_bytes_per_launch"] == pytest.approx(d["fetch_bytes_per_launch"] + d["write_bytes_per_launch"])
     src = d["source"].split(":")[0]
     assert os.path.isdir(os.path.join(REPO, src)), src
+
+
+def test_valu_ceiling_summary_is_committed_and_consistent():
+    """profiles/valu_peak.json: its session is committed; the per-SIMD v_fma_f32 rates grow with occupancy
+    up to at most the spec's 0.5 per SIMD-cycle; the counter-derived rate of each measured launch (GRBM
+    cycles, the method bench.py applies to the bake) agrees with the per-SIMD stamps"""
+    d = json.load(open(os.path.join(REPO, "profiles", "valu_peak.json")))
+    src = d["source"].split("/valu.log")[0]
+    assert os.path.isdir(os.path.join(REPO, src)), src
+    by = {int(k): v for k, v in d["f32_per_simd_per_clk_by_waves"].items()}
+    assert by[1] < by[2] <= max(by.values()) <= d["spec_fma_per_simd_cycle"] == pytest.approx(0.5, rel=0.01)
+    for w, c in d["counters"]["fma64"].items():
+        assert c["valu_per_simd_cycle"] == pytest.approx(by[int(w)], rel=0.05), (w, c)

@@ -4,7 +4,8 @@ Each rank plans the reference schedule with the product's host-only context (fmg
 launches, rng offsets and work items on every rank), takes its shard (fmgi.parallel.shard_range) and
 bakes it -- with the oracle standing in for the GPU, since this container has none -- and the int64
 lightmaps are summed with fmgi.parallel.reduce_lightmap (the same call bench.py makes over RCCL). The
-reduced lightmap must equal the single-process bake bit for bit. The drop-in's own one-process layout for
+reduced lightmap must equal the single-process bake bit for bit, and fmgi.parallel.gather_rows (bench.py's
+per-rank breakdown at N > 1) must hand every rank all ranks' rows in rank order. The drop-in's own one-process layout for
 8 GPUs (fmgi_dropin_shards, fmgi_dropin_reduce_order: the peer-copy tree used without RCCL) is replayed
 on per-shard lightmaps the same way."""
 import os
@@ -49,6 +50,11 @@ def _worker(rank, world, port, items, out_path):
     lm = torch.zeros((sc.num_texels, 4), dtype=torch.int64)
     lm[:, :3] = torch.from_numpy(lm3)
     parallel.reduce_lightmap(lm, dst=0)
+    # bench.py's per-rank breakdown: every rank's row, in rank order, on every rank (exact in float64)
+    rows = parallel.gather_rows([rank, b, e, 100 * (e - b) + 0.5])
+    assert rows == [[float(r), *map(float, parallel.shard_range(items, r, world)),
+                     100.0 * (parallel.shard_range(items, r, world)[1] - parallel.shard_range(items, r, world)[0]) + 0.5]
+                    for r in range(world)], rows
     if rank == 0:
         np.save(out_path, lm.numpy())
     dist.barrier()

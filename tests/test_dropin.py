@@ -7,7 +7,10 @@ synthetic two-room layout PNG made here. It parses the layout, calls our perform
 Expected: the same geometry (the reference parser, oracle/_ref/dump_geometry), baked through the
 library's non-mutating entry point from the same libc rand() state and run through fmgi_output_tiles
 (byte-identical to the reference's saveAs, tests/test_output.py). Every tile PNG must match byte for
-byte. The layout is generated (no reference data file is used)."""
+byte, and the program's console output carries the reference's per-launch progress lines
+(global_illumination_cl.c:248-249, one "\rphoton-mapping window with %d M samples   " per launch with the
+samples still to launch for that source, a newline after each source). The layout is generated (no
+reference data file is used)."""
 import ctypes
 import os
 import subprocess
@@ -15,6 +18,7 @@ import subprocess
 import numpy as np
 import pytest
 
+import fm_oracle as O
 from conftest import REPO
 
 REF = os.path.join(REPO, "oracle", "_ref")
@@ -57,11 +61,23 @@ def test_reference_cli_linked_against_library(torch_cuda, tmp_path):
     assert len(sc.walls) > 10 and len(sc.windows) == 1 and len(sc.lights) >= 1
 
     os.makedirs(tmp_path / "tiles")
-    env = dict(os.environ, FMGI_QUIET="1")
-    run = subprocess.run([PROG, png], cwd=tmp_path, env=env, capture_output=True, text=True, timeout=300)
-    assert run.returncode == 0, run.stdout[-2000:] + run.stderr[-2000:]
+    env = {k: v for k, v in os.environ.items() if k != "FMGI_QUIET"}
+    run = subprocess.run([PROG, png], cwd=tmp_path, env=env, capture_output=True, timeout=300)
+    out = run.stdout.decode(errors="replace")  # bytes: text mode would turn the "\r"s into newlines
+    assert run.returncode == 0, out[-2000:] + run.stderr.decode(errors="replace")[-2000:]
 
     spa = 1000 * 1000 * 100  # main.c:58
+    sched = O.schedule_with_offsets(sc, spa, np.zeros(4096, np.int32))
+    progress = ""
+    for s_idx in range(len(sc.windows) + len(sc.lights)):
+        counts = [int(c) for c in sched["count"][sched["source"] == s_idx]]
+        left = sum(counts)
+        for c in counts:
+            progress += "\rphoton-mapping window with %d M samples   " % (left * 100 // 1000000)
+            left -= c
+        progress += "\n"
+    assert "[INF] Selected device '" in out
+    assert progress in out, out[-2000:]
     libc = ctypes.CDLL(None)
     libc.srand(1)  # the CLI process starts from glibc's unseeded state
     tex = fmgi.bake_geometry(sc, spa, np.zeros((sc.num_texels, 4), np.float32))

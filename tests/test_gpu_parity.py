@@ -118,9 +118,9 @@ def test_box_traces_without_axes_mode(torch_cuda, box200, offsets):
 
 
 def test_layout_traces_with_floor_plan(torch_cuda, example_scene, offsets):
-    """The hybrid scan's walls through its filter pass (default: nearest-first classes, wave-uniform early
-    exit) and through the floor-plan walk (FMGI_PLAN=1, plan_walls): both give the oracle's traces and
-    lightmap."""
+    """The hybrid scan's walls through the packed wall-pair filter (default, FMGI_FILTER_PK=1:
+    filter_pairs over the pair image) and through the floor-plan walk (FMGI_PLAN=1, plan_walls): both
+    give the oracle's traces and lightmap."""
     spa = 6_500_000
     L = _oracle_plan(example_scene, spa, offsets)
     ctx = _ctx(example_scene, spa, offsets)

@@ -8,6 +8,7 @@
 #   tol              whole-launch reference sums, strict and relaxed (tests/golden/make_tolerance_fixtures.py)
 #   ocml             the device library's sin/cos digest (tests/golden/make_ocml_fixture.py)
 #   valu             VALU issue ceilings (tools/valu_peak)
+#   valupmc          the same cases' SQ issue counters (one rocprofv3 --pmc pass per case, 1/2/4/8 waves)
 #   dropin           drop-in boundary timing, cached and uncached (tools/bench_dropin.py)
 #   dropinprof       the same under rocprofv3 --kernel-trace --stats
 #   bench            python bench.py $BENCH_ARGS
@@ -21,6 +22,7 @@
 #   foldpmc          one rocprofv3 --pmc pass of LDS-pipe counters (the fold kernels' binding resource)
 #   sq               two rocprofv3 --pmc passes of SQ instruction / wait counters ($PROF_ARGS)
 #   grbm / tcp / sq3 one --pmc pass each: GRBM clock + SQ cycle split / TA-TD-TCP (vector memory path) / SQ memory issue
+#   rehearse         bench.py's N-rank path with REHEARSE_N (default 2) gloo ranks sharing the box's one GPU
 #   clock            bench with the in-kernel clock build (make -C <pkg> variant VNAME=clock VFLAGS=-DFMGI_CLOCK_STAMP)
 # Each GPU step has its own time limit; a crash/timeout (rc > 1) stops the session.
 set -u
@@ -47,7 +49,10 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;
     tol)   step tol 1100 env GPU_MAX_HW_QUEUES=16 python -u tests/golden/make_tolerance_fixtures.py "$OUT" ;;
     ocml)  step ocml 300 python tests/golden/make_ocml_fixture.py "$OUT" ;;
-    valu)  step valu 120 ./tools/valu_peak ;;
+    valu)  step valu 300 ./tools/valu_peak ;;
+    valupmc) for c in fma8 fma64 pk_fma64 fma64_salu64; do
+               step "valupmc_$c" 120 rocprofv3 --pmc SQ_INSTS_VALU SQ_ACTIVE_INST_VALU SQ_INSTS_SALU SQ_ACTIVE_INST_ANY SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES GRBM_GUI_ACTIVE -d "$OUT/valupmc_$c" -o run --output-format csv -- ./tools/valu_peak $c 1,2,4,8 --ms 20 || exit $?
+             done ;;
     dropin) step dropin 600 python tools/bench_dropin.py && step dropin_nocache 600 python tools/bench_dropin.py --no-cache ;;
     dropinprof) step dropinprof 600 rocprofv3 --kernel-trace --stats -d "$OUT/dropinprof" -o run --output-format csv -- python tools/bench_dropin.py --reps 2 ;;
     bench) step bench 600 python bench.py ${BENCH_ARGS:-} ;;
@@ -66,6 +71,7 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     grbm)  step grbm 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$OUT/grbm" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     tcp)   step tcp 600 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum GRBM_GUI_ACTIVE -d "$OUT/tcp" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     sq3)   step sq3 600 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA -d "$OUT/sq3" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    rehearse) step rehearse 600 env FMGI_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node ${REHEARSE_N:-2} --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus ${REHEARSE_N:-2} --steps 3 --warmup 1 --no-cpu-baseline ;;
     clock) step clock 600 env FMGI_LIB=clock python bench.py --steps 5 --warmup 3 --no-cpu-baseline ${PROF_ARGS:-} ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
