@@ -267,7 +267,9 @@ __device__ __forceinline__ void filter_axis(const char *img, int J, int sub, int
  * per iteration in packed fp32. A group holds records 2g and 2g + 1 of a class as field pairs, so each
  * pair is a 64-bit register pair straight from ds_read_b128, and fac', the two hit coordinates and their
  * offsets from the records' centres run as v_pk_add_f32 / v_pk_mul_f32 / v_pk_fma_f32: two fp32 ops per
- * lane per issue slot (the f32 VALU peak on gfx950 is v_pk_fma_f32's, MI355X_MICROARCH.md). Each element
+ * lane per instruction, but each occupies the SIMD for 4 cycles, as two v_fma_f32 do (tools/valu_peak.hip,
+ * profiles/valu_peak.json: 0.24 v_pk_fma_f32 vs 0.45 v_fma_f32 per SIMD-cycle); the gain is fewer
+ * instructions to issue and the 64-bit operand pairs read straight from ds_read_b128. Each element
  * is the same IEEE op on the same operands as filter_axis's, so every key and candidate test is
  * filter_axis's bit for bit; the compares and the (L1, L2, code1) update stay per record, in record
  * order. code1 receives the record's rect index itself (loaded with the fields), not a position.
@@ -1264,6 +1266,9 @@ struct AccStream {
         if (fill + n < FMGI_RING_CODES) return;
         /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
         const int presort = uni(a.presort);
+#ifdef FMGI_EXP_NOFLUSH /* PROFILING ONLY: the ring wraps without being written out (the lightmap is lost) */
+        if (presort < 0)
+#endif
         if (presort == 2) bucket_out(a, ring, FMGI_RING_CODES);
         else if (presort) sorted_out(a, ws, ring, FMGI_RING_CODES);
         else copy_out(a, ws, ring, FMGI_RING_CODES);

@@ -6,7 +6,12 @@
             memory-sized stream chunks) -- size-independent properties (chunk and split invariance,
             photon / scan / deposit accounting, no stream overflow) plus an exact oracle window taken
             from the schedule's LAST launches, whose rng offsets lie deep in the glibc prefix
-  config 5  box2000: a 1e7-photon prefix against the oracle for every scan and accumulation mode
+  config 3  box200, spa 172,413,793: the whole 1,000,012,800-photon lightmap (the bench's step) against
+            the oracle's FMA port (bit-identical to the oracle) on the host's threads, bit for bit (~190 s
+            on the GPU box's 16 threads)
+  config 5  box2000: a 1e7-photon prefix against the oracle for every scan and accumulation mode, and at
+            full size (1e9 photons) split, chunk and accumulation-mode invariance, photon / scan / deposit
+            accounting and the last launch's items against the oracle
   apartment30 (654 walls, 34 sources; the grid's per-axis walk with binary search and records-box
             skip): per-photon traces and a lightmap prefix against the oracle
 """
@@ -89,6 +94,73 @@ def test_config2_full_lightmap_exact(torch_cuda, example_scene, offsets):
     # (3 items per lane: the reordered fetch table is in use) and must give the same bits
     lm2 = _bake_gpu(torch_cuda, ctx, 0, n)
     assert np.array_equal(lm2, lm)
+    ctx.close()
+
+
+def _host_threads():
+    return int(os.environ.get("OMP_NUM_THREADS", "0") or 0) or min(os.cpu_count() or 1, 16)
+
+
+@pytest.mark.timeout(900)
+def test_config3_full_lightmap_exact(torch_cuda, box200, offsets):
+    """BASELINE config 3 -- the headline bench's step -- at full size: all 10,000,128 work items
+    (1,000,012,800 photons, 391 launches) through the default path (closed-box grid scan, bucketed stream,
+    one chunk), the whole int64 lightmap and the photon / scan / deposit / escape counters equal to the
+    oracle's FMA port bit for bit."""
+    spa = 172_413_793
+    L = O.schedule_with_offsets(box200, spa, offsets)
+    assert len(L) == 391
+    ctx = _ctx(box200, spa, offsets)
+    assert ctx.get_plan().tobytes() == L.tobytes()
+    n = ctx.total_items
+    assert 100 * n == 1_000_012_800
+    ctx.reset_stats()
+    lm = _bake_gpu(torch_cuda, ctx, 0, n)
+    st = ctx.stats()
+    ctx.close()
+    assert st["stream_overflow"] == 0
+    olm, ost = O.bake_port(box200, L, 0, n, nthreads=_host_threads())
+    assert np.array_equal(lm[:, :3], olm)
+    assert not lm[:, 3].any()
+    for k in ("photons", "scans", "deposits", "escapes"):
+        assert st[k] == ost[k], k
+
+
+@pytest.mark.timeout(600)
+def test_config5_full_size_properties_and_late_window(torch_cuda, box2000, offsets):
+    """BASELINE config 5 (box2000, 1e9 photons: the LDS-spilling scene) at full size: the default bake
+    equals the sum of two halves baked in forced memory-sized chunks and the FX3-atomics bake (exact
+    integer sums are order- and mode-free), the counters account for every photon, and the last
+    launch's final 1,024 items equal the oracle exactly."""
+    spa = 172_413_793
+    L = O.schedule_with_offsets(box2000, spa, offsets)
+    ctx = _ctx(box2000, spa, offsets)
+    assert ctx.get_plan().tobytes() == L.tobytes()
+    n = ctx.total_items
+    assert 100 * n >= 1_000_000_000
+    ctx.reset_stats()
+    full = _bake_gpu(torch_cuda, ctx, 0, n)
+    st = ctx.stats()
+    assert st["photons"] == 100 * n
+    assert st["deposits"] + st["escapes"] == st["scans"]
+    assert st["stream_overflow"] == 0
+    assert st["exact_rescans"] > 0
+    os.environ["FMGI_CHUNK_ITEMS"] = "1700000"  # ~3 chunks per half
+    try:
+        h1 = _bake_gpu(torch_cuda, ctx, 0, n // 2)
+        h2 = _bake_gpu(torch_cuda, ctx, n // 2, n)
+    finally:
+        os.environ.pop("FMGI_CHUNK_ITEMS", None)
+    assert np.array_equal(full, h1 + h2)
+    ctx.close()
+    fx = _ctx(box2000, spa, offsets, fmgi.ACCUM_FX3)
+    assert np.array_equal(full, _bake_gpu(torch_cuda, fx, 0, n))
+    fx.close()
+    b = n - 1024
+    assert int(L[-1]["item_begin"]) < b
+    olm, _ = O.bake_port(box2000, L, b, n, nthreads=_host_threads())
+    ctx = _ctx(box2000, spa, offsets)
+    assert np.array_equal(_bake_gpu(torch_cuda, ctx, b, n)[:, :3], olm)
     ctx.close()
 
 
