@@ -1367,6 +1367,19 @@ static uint64_t stream_chunk_items(fmgi_context *c, int sets, int mode) {
     return std::max<uint64_t>(items, 65536);
 }
 
+/* the stream layout of a STREAM bake: per-wave tile buckets (the bake's ring flush sorts by fold tile and
+   appends each tile's run to the wave's bucket of that tile; the fold reads whole blocks) when the tiles
+   fit one histogram entry per lane, else unsorted codes + k_slice_sort. FMGI_PRESORT=0/1/2 forces unsorted /
+   presorted segments / buckets. */
+static int stream_layout(const fmgi_context *c) {
+    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
+    const char *pre_env = getenv("FMGI_PRESORT");
+    int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamBuckets : kStreamSliced;
+    if (pre_env && P >= 1 && P <= FMGI_PRESORT_MAX_TILES) smode = std::max(0, std::min(2, atoi(pre_env)));
+    if (pre_env && atoi(pre_env) == 0) smode = kStreamSliced;
+    return smode;
+}
+
 static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
                        void *events, int32_t *counts, uint32_t *rngf) {
     if (!c || !lm) return set_err(FMGI_ERR_ARG, "fmgi_bake_items: bad arguments");
@@ -1376,6 +1389,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
                                                   (unsigned long long)c->total_items);
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_HYBRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     const bool was_auto = kernel == FMGI_KERNEL_AUTO;
+    /* the kernel instance's accumulation: the bucket layout of the stream has its own (kAccBucket) */
+    const int kacc = (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamBuckets) ? kAccBucket : c->accum;
     if (was_auto) kernel = c->auto_kernel;
     kernel = fitting_kernel(c, kernel, c->accum, bake_block()); /* an image too large for LDS: same results, other scan */
     if (b == e) return FMGI_OK;
@@ -1384,12 +1399,12 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
        hybrid bake vs ~3.5 ms cooperative) */
     if (was_auto && kernel == FMGI_KERNEL_HYBRID && !trace && c->accum == FMGI_ACCUM_STREAM &&
         fitting_kernel(c, FMGI_KERNEL_FAST, c->accum, bake_block()) == FMGI_KERNEL_FAST) {
-        const StagePlan fp = plan_stage(c, FMGI_KERNEL_FAST, c->accum, trace);
+        const StagePlan fp = plan_stage(c, FMGI_KERNEL_FAST, kacc, trace);
         const uint64_t lanes_max =
-            (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, c->accum, trace, fp.block, fp.bytes, UINT64_MAX) * fp.block;
+            (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, kacc, trace, fp.block, fp.bytes, UINT64_MAX) * fp.block;
         if ((e - b) * 2 <= lanes_max) kernel = FMGI_KERNEL_FAST;
     }
-    const StagePlan sp = plan_stage(c, kernel, c->accum, trace);
+    const StagePlan sp = plan_stage(c, kernel, kacc, trace);
     const int block = sp.block;
     if (c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     /* no walls: every photon escapes at its first scan (photonmap.cl:208), so nothing is deposited */
@@ -1495,7 +1510,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     a.ev_counts = counts;
     a.rng_final = rngf;
     a.overflow = c->d_stats + KSTAT_OVERFLOW;
-    fmgi_bake_lds(kernel, c->accum, block, a.fimg_bytes, &a.ring_off);
+    fmgi_bake_lds(kernel, kacc, block, a.fimg_bytes, &a.ring_off);
     /* lanes per work item: a launch with fewer items than resident lanes (BASELINE config 1 has 11,008)
        gives each item a group of up to 8 lanes that split every ScanFast scan's records, so the idle
        lanes shorten the items' serial photon chains (FMGI_COOP forces a group size: tests) */
@@ -1506,7 +1521,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             a.coop = (k == 2 || k == 4 || k == 8) ? k : 1;
         } else {
             const uint64_t lanes_max =
-                (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block;
+                (uint64_t)grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, UINT64_MAX) * block;
             while (a.coop < 8 && (e - b) * (uint64_t)a.coop * 2 <= lanes_max) a.coop *= 2;
         }
         if (a.coop > 1) kernel = FMGI_KERNEL_FAST_COOP;
@@ -1523,7 +1538,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int ns = c->nsrcs;
     /* only launches of at most 16 items per resident lane reorder (box200's 30 per lane: plain order) */
     const uint64_t order_lanes =
-        order_on ? (uint64_t)grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block /
+        order_on ? (uint64_t)grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, UINT64_MAX) * block /
                        (uint64_t)a.coop
                  : 0;
     if (order_on) {
@@ -1620,8 +1635,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), c->accum, trace,
-                                grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop),
+        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), kacc, trace,
+                                grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop),
                                 block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
@@ -1638,18 +1653,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
        and bake occupancy tried, because the persistent bake leaves the folds no room to run beside it,
        so the default is 1. */
     const uint64_t n = e - b;
-    const int lanes = grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, UINT64_MAX) * block;
+    const int lanes = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, UINT64_MAX) * block;
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
-    /* the stream layout: per-wave tile buckets (the bake's ring flush sorts by fold tile and appends each
-       tile's run to the wave's bucket of that tile; the fold reads whole blocks) when the tiles fit one
-       histogram entry per lane, else unsorted codes + k_slice_sort. FMGI_PRESORT=0/1/2 forces unsorted /
-       presorted segments / buckets. */
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
-    const char *pre_env = getenv("FMGI_PRESORT");
-    int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamBuckets : kStreamSliced;
-    if (pre_env && P >= 1 && P <= FMGI_PRESORT_MAX_TILES) smode = std::max(0, std::min(2, atoi(pre_env)));
-    if (pre_env && atoi(pre_env) == 0) smode = kStreamSliced;
+    const int smode = stream_layout(c); /* kStreamBuckets <=> kacc == kAccBucket */
     uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, smode);
     if (const char *ce = getenv("FMGI_CHUNK_ITEMS")) /* tests: force several chunks */
         if (atoll(ce) > 0) chunk = std::min<uint64_t>(chunk, (uint64_t)atoll(ce));
@@ -1668,7 +1676,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
         const int k = overlap ? (nchunk & 1) : 0; /* one buffer set unless the folds run beside the bakes */
-        const int grid = grid_blocks(c, kernel, c->accum, trace, block, a.fimg_bytes, (ce - cb) * (uint64_t)a.coop);
+        const int grid = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (ce - cb) * (uint64_t)a.coop);
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));
@@ -1699,7 +1707,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), c->accum, trace, grid, block, s));
+        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), kacc, trace, grid, block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         if (overlap) {
             HIPCHK(hipEventRecord(c->ev_baked[k], s));

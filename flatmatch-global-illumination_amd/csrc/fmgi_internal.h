@@ -135,7 +135,9 @@ enum { KSTAT_PHOTONS = 0, KSTAT_SCANS, KSTAT_DEPOSITS, KSTAT_ESCAPES, KSTAT_RESC
 
 /* stream accumulation geometry (fmgi_accum.hip) */
 #define FMGI_STREAM_BLOCK 4096 /* codes reserved per wave at a time                         */
+#ifndef FMGI_RING_CODES        /* (experiment builds: make fullvariant)                     */
 #define FMGI_RING_CODES 1024   /* codes a wave collects in LDS before writing them out       */
+#endif
 static_assert(FMGI_STREAM_BLOCK % FMGI_RING_CODES == 0, "ring flushes must tile the stream blocks");
 #define FMGI_STREAM_SLICE 8192 /* codes per histogram / scatter block                        */
 #define FMGI_STREAM_SLICE_BIG 32768 /* ... for lightmaps of more than 128 fold tiles                */
@@ -177,7 +179,10 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
 /* internal kernel id (not in the C ABI): ScanFast with BakeArgs::coop lanes per work item */
 #define FMGI_KERNEL_FAST_COOP 101
 
-/* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only), 4 = AccStream */
+/* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only), 4 = AccStream (unsorted / presorted
+   stream layouts), kAccBucket = AccBucket (the stream in the per-tile bucket layout, BakeArgs::presort 2:
+   its own kernel instance) */
+constexpr int kAccBucket = 5;
 /* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
    FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */
 #define FMGI_KVAR_AXES 0x100

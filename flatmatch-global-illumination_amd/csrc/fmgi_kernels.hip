@@ -946,7 +946,12 @@ struct WaveStream {
     uint32_t tot = 0;           /* codes appended; the ring holds tot % FMGI_RING_CODES of them */
 };
 
-struct AccStream {
+/* Mode: the stream layout, fixed at compile time (2 = per-tile buckets, the default layout: the kernel
+   instance then holds no code and no registers for the other layouts' block cursor and copies) or read
+   from BakeArgs::presort (-1: unsorted codes or presorted segments) */
+template <int Mode>
+struct AccStreamT {
+    static __device__ __forceinline__ int layout(const BakeArgs &a) { return Mode >= 0 ? Mode : uni(a.presort); }
     static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
 
     /* a fresh global block for the wave (every live lane learns it) */
@@ -993,7 +998,8 @@ struct AccStream {
         for (uint32_t k = r; k < 64; k += nl) hist[k] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        const bool full = nl == 64 && n == FMGI_RING_CODES; /* every lane owns 16 consecutive codes */
+        /* every lane owns 16 consecutive codes (1024-code rings) */
+        const bool full = nl == 64 && n == FMGI_RING_CODES && FMGI_RING_CODES == 1024;
         uint32_t cr[16]; /* full: the lane's codes, held while the ring is overwritten in sorted order */
         if (full) {
             const uint4 *rq = (const uint4 *)ring + 4 * r;
@@ -1164,21 +1170,24 @@ struct AccStream {
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
         if (nl == 64) {
-            uint32_t cr[16];
+            constexpr int CPL = FMGI_RING_CODES / 64; /* codes per lane of a full ring */
+            static_assert(CPL % 4 == 0, "rings of a multiple of 256 codes");
+            constexpr int SC = CPL < 8 ? CPL : 8;     /* scatter group */
+            uint32_t cr[CPL];
             if (n == FMGI_RING_CODES) {
-                const uint4 *rq = (const uint4 *)ring + 4 * r;
+                const uint4 *rq = (const uint4 *)ring + (CPL / 4) * r;
 #pragma unroll
-                for (int h = 0; h < 4; h++) {
+                for (int h = 0; h < CPL / 4; h++) {
                     const uint4 c = rq[h];
                     cr[4 * h] = c.x, cr[4 * h + 1] = c.y, cr[4 * h + 2] = c.z, cr[4 * h + 3] = c.w;
                 }
             } else {
 #pragma unroll
-                for (int e = 0; e < 16; e++) cr[e] = 16 * r + e < n ? ring[16 * r + e] : kSent;
+                for (int e = 0; e < CPL; e++) cr[e] = CPL * r + e < n ? ring[CPL * r + e] : kSent;
             }
             const uint32_t ov = ring[FMGI_RING_CODES + r]; /* the overflow (append moves it after the flush) */
 #pragma unroll
-            for (int e = 0; e < 16; e++)
+            for (int e = 0; e < CPL; e++)
                 if (cr[e] != kSent) atomicAdd(&hist[cr[e] >> shift], 1u);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1194,13 +1203,13 @@ struct AccStream {
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
-            for (int h = 0; h < 16; h += 8) {
-                uint32_t o[8];
+            for (int h = 0; h < CPL; h += SC) {
+                uint32_t o[SC];
 #pragma unroll
-                for (int e = 0; e < 8; e++)
+                for (int e = 0; e < SC; e++)
                     o[e] = cr[h + e] != kSent ? atomicAdd(&hist[cr[h + e] >> shift], 1u) : 0u;
 #pragma unroll
-                for (int e = 0; e < 8; e++)
+                for (int e = 0; e < SC; e++)
                     if (cr[h + e] != kSent) ring[o[e]] = cr[h + e];
             }
             for (uint32_t k = cnt; k < pc; k++) ring[start + k] = kSent;
@@ -1265,7 +1274,7 @@ struct AccStream {
         ws.tot += n;
         if (fill + n < FMGI_RING_CODES) return;
         /* the ring is full: write out its first FMGI_RING_CODES codes, keep the (< 64) rest at its start */
-        const int presort = uni(a.presort);
+        const int presort = layout(a);
 #ifdef FMGI_EXP_NOFLUSH /* PROFILING ONLY: the ring wraps without being written out (the lightmap is lost) */
         if (presort < 0)
 #endif
@@ -1294,7 +1303,7 @@ struct AccStream {
         ws.end = __shfl(ws.end, src, 64);
         const uint32_t fill = ws.tot % FMGI_RING_CODES, padded = (fill + 3) & ~3u;
         const uint32_t lane = __lane_id();
-        if (a.presort == 2) { /* the last (partial) ring into the buckets, then close them */
+        if (layout(a) == 2) { /* the last (partial) ring into the buckets, then close them */
             if (fill) bucket_out(a, ring, fill);
             bucket_close(a, ring);
             return;
@@ -1312,12 +1321,15 @@ struct AccStream {
     }
 };
 
+using AccStream = AccStreamT<-1>; /* unsorted codes / presorted segments (BakeArgs::presort 0, 1) */
+using AccBucket = AccStreamT<2>;  /* per-tile buckets (BakeArgs::presort 2) */
+
 template <class Acc>
 struct HasAppend {
     static constexpr bool value = false;
 };
-template <>
-struct HasAppend<AccStream> {
+template <int Mode>
+struct HasAppend<AccStreamT<Mode>> {
     static constexpr bool value = true;
 };
 
@@ -1396,7 +1408,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         __syncthreads();
     }
     if constexpr (HasAppend<Acc>::value)
-        if (a.presort == 2) AccStream::bucket_init(a, ring);
+        if (Acc::layout(a) == 2) Acc::bucket_init(a, ring);
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
@@ -1552,7 +1564,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         depth++;
         }
         sst.clk.lap(ST_HIT);
-        if constexpr (HasAppend<Acc>::value) AccStream::append(a, ws, ring, dep && lead, code);
+        if constexpr (HasAppend<Acc>::value) Acc::append(a, ws, ring, dep && lead, code);
         sst.clk.lap(ST_APPEND);
     }
 #ifdef FMGI_CLOCK_STAMP /* sum over waves of the shader-clock and 100-MHz deltas of the loop: stats[24], [25] */
@@ -1564,7 +1576,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         }
     }
 #endif
-    if constexpr (HasAppend<Acc>::value) AccStream::finish(a, ws, ring);
+    if constexpr (HasAppend<Acc>::value) Acc::finish(a, ws, ring);
     if (TRACE && photon >= 0) {
         a.ev_counts[item - a.item_begin] = nev;
         a.rng_final[item - a.item_begin] = rng;
@@ -1753,43 +1765,36 @@ const void *kernel_ptr(bool trace) {
     return trace ? (const void *)&k_bake<Scan, Acc, true> : (const void *)&k_bake<Scan, Acc, false>;
 }
 
+/* accumulation codes: FMGI_ACCUM_FX3 1, STATE 2, NONE 3, STREAM 4 (unsorted / presorted layouts) and the
+   internal kAccBucket 5 (STREAM in the per-tile bucket layout) */
+template <class Scan>
+const void *kernel_acc(int accum, bool trace) {
+    if (accum == 2) return kernel_ptr<Scan, AccState>(trace);
+    if (accum == 3) return kernel_ptr<Scan, AccNone>(trace);
+    if (accum == 4) return kernel_ptr<Scan, AccStream>(trace);
+    if (accum == kAccBucket) return kernel_ptr<Scan, AccBucket>(trace);
+    return kernel_ptr<Scan, AccFx3>(trace);
+}
+
+template <class Scan>
+void launch_acc(const BakeArgs &a, int accum, bool trace, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+    if (accum == 2) launch3<Scan, AccState>(a, trace, grid, block, lds, s);
+    else if (accum == 3) launch3<Scan, AccNone>(a, trace, grid, block, lds, s);
+    else if (accum == 4) launch3<Scan, AccStream>(a, trace, grid, block, lds, s);
+    else if (accum == kAccBucket) launch3<Scan, AccBucket>(a, trace, grid, block, lds, s);
+    else launch3<Scan, AccFx3>(a, trace, grid, block, lds, s);
+}
+
 const void *bake_kernel(int kernel, int accum, bool trace) {
-    if (kernel == (2 | FMGI_KVAR_AXES)) {
-        if (accum == 2) return kernel_ptr<ScanGridAxes, AccState>(trace);
-        if (accum == 3) return kernel_ptr<ScanGridAxes, AccNone>(trace);
-        if (accum == 4) return kernel_ptr<ScanGridAxes, AccStream>(trace);
-        return kernel_ptr<ScanGridAxes, AccFx3>(trace);
-    }
-    if (kernel == (4 | FMGI_KVAR_PLAN)) {
-        if (accum == 2) return kernel_ptr<ScanHybridPlan, AccState>(trace);
-        if (accum == 3) return kernel_ptr<ScanHybridPlan, AccNone>(trace);
-        if (accum == 4) return kernel_ptr<ScanHybridPlan, AccStream>(trace);
-        return kernel_ptr<ScanHybridPlan, AccFx3>(trace);
-    }
+    if (kernel == FMGI_KERNEL_FAST_COOP)
+        return accum == kAccBucket ? kernel_ptr<ScanFastCoop, AccBucket>(false) : kernel_ptr<ScanFastCoop, AccStream>(false);
+    if (kernel == (2 | FMGI_KVAR_AXES)) return kernel_acc<ScanGridAxes>(accum, trace);
+    if (kernel == (4 | FMGI_KVAR_PLAN)) return kernel_acc<ScanHybridPlan>(accum, trace);
     kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN);
-    if (kernel == 2) {
-        if (accum == 2) return kernel_ptr<ScanGrid, AccState>(trace);
-        if (accum == 3) return kernel_ptr<ScanGrid, AccNone>(trace);
-        if (accum == 4) return kernel_ptr<ScanGrid, AccStream>(trace);
-        return kernel_ptr<ScanGrid, AccFx3>(trace);
-    }
-    if (kernel == FMGI_KERNEL_FAST_COOP) return kernel_ptr<ScanFastCoop, AccStream>(false);
-    if (kernel == 4) {
-        if (accum == 2) return kernel_ptr<ScanHybrid, AccState>(trace);
-        if (accum == 3) return kernel_ptr<ScanHybrid, AccNone>(trace);
-        if (accum == 4) return kernel_ptr<ScanHybrid, AccStream>(trace);
-        return kernel_ptr<ScanHybrid, AccFx3>(trace);
-    }
-    if (kernel == 1) {
-        if (accum == 2) return kernel_ptr<ScanFast, AccState>(trace);
-        if (accum == 3) return kernel_ptr<ScanFast, AccNone>(trace);
-        if (accum == 4) return kernel_ptr<ScanFast, AccStream>(trace);
-        return kernel_ptr<ScanFast, AccFx3>(trace);
-    }
-    if (accum == 2) return kernel_ptr<ScanExact, AccState>(trace);
-    if (accum == 3) return kernel_ptr<ScanExact, AccNone>(trace);
-    if (accum == 4) return kernel_ptr<ScanExact, AccStream>(trace);
-    return kernel_ptr<ScanExact, AccFx3>(trace);
+    if (kernel == 2) return kernel_acc<ScanGrid>(accum, trace);
+    if (kernel == 4) return kernel_acc<ScanHybrid>(accum, trace);
+    if (kernel == 1) return kernel_acc<ScanFast>(accum, trace);
+    return kernel_acc<ScanExact>(accum, trace);
 }
 
 } // namespace
@@ -1801,7 +1806,7 @@ int fmgi_kernels_filter_pk() { return FMGI_FILTER_PK; }
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
-    return img + (accum == 4 ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
+    return img + ((accum == 4 || accum == kAccBucket) ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
 
 /* a bake launch of more than 64 KiB of dynamic LDS (scan image + staged tables + rings, fmgi_api.cpp
@@ -1841,38 +1846,21 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         if (e != hipSuccess) return e;
     }
     if (kernel == FMGI_KERNEL_FAST_COOP) {
-        if (accum != 4 || trace) return hipErrorInvalidValue; /* cooperative lanes: stream accumulation only */
-        launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
+        if ((accum != 4 && accum != kAccBucket) || trace) return hipErrorInvalidValue; /* stream accumulation only */
+        if (accum == kAccBucket) launch3<ScanFastCoop, AccBucket>(a, false, grid, blk, lds, s);
+        else launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
     } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */
-        if (accum == 2) launch3<ScanHybridPlan, AccState>(a, trace, grid, blk, lds, s);
-        else if (accum == 3) launch3<ScanHybridPlan, AccNone>(a, trace, grid, blk, lds, s);
-        else if (accum == 4) launch3<ScanHybridPlan, AccStream>(a, trace, grid, blk, lds, s);
-        else launch3<ScanHybridPlan, AccFx3>(a, trace, grid, blk, lds, s);
+        launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
-        if (accum == 2) launch3<ScanHybrid, AccState>(a, trace, grid, blk, lds, s);
-        else if (accum == 3) launch3<ScanHybrid, AccNone>(a, trace, grid, blk, lds, s);
-        else if (accum == 4) launch3<ScanHybrid, AccStream>(a, trace, grid, blk, lds, s);
-        else launch3<ScanHybrid, AccFx3>(a, trace, grid, blk, lds, s);
+        launch_acc<ScanHybrid>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES)) { /* FMGI_KERNEL_GRID, closed box */
-        if (accum == 2) launch3<ScanGridAxes, AccState>(a, trace, grid, blk, lds, s);
-        else if (accum == 3) launch3<ScanGridAxes, AccNone>(a, trace, grid, blk, lds, s);
-        else if (accum == 4) launch3<ScanGridAxes, AccStream>(a, trace, grid, blk, lds, s);
-        else launch3<ScanGridAxes, AccFx3>(a, trace, grid, blk, lds, s);
+        launch_acc<ScanGridAxes>(a, accum, trace, grid, blk, lds, s);
     } else if ((kernel & ~FMGI_KVAR_AXES) == 2) { /* FMGI_KERNEL_GRID */
-        if (accum == 2) launch3<ScanGrid, AccState>(a, trace, grid, blk, lds, s);
-        else if (accum == 3) launch3<ScanGrid, AccNone>(a, trace, grid, blk, lds, s);
-        else if (accum == 4) launch3<ScanGrid, AccStream>(a, trace, grid, blk, lds, s);
-        else launch3<ScanGrid, AccFx3>(a, trace, grid, blk, lds, s);
+        launch_acc<ScanGrid>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == 1) { /* FMGI_KERNEL_FAST */
-        if (accum == 2) launch3<ScanFast, AccState>(a, trace, grid, blk, lds, s);
-        else if (accum == 3) launch3<ScanFast, AccNone>(a, trace, grid, blk, lds, s);
-        else if (accum == 4) launch3<ScanFast, AccStream>(a, trace, grid, blk, lds, s);
-        else launch3<ScanFast, AccFx3>(a, trace, grid, blk, lds, s);
+        launch_acc<ScanFast>(a, accum, trace, grid, blk, lds, s);
     } else {
-        if (accum == 2) launch3<ScanExact, AccState>(a, trace, grid, blk, lds, s);
-        else if (accum == 3) launch3<ScanExact, AccNone>(a, trace, grid, blk, lds, s);
-        else if (accum == 4) launch3<ScanExact, AccStream>(a, trace, grid, blk, lds, s);
-        else launch3<ScanExact, AccFx3>(a, trace, grid, blk, lds, s);
+        launch_acc<ScanExact>(a, accum, trace, grid, blk, lds, s);
     }
     return hipGetLastError();
 }
