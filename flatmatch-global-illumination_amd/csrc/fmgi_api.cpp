@@ -1284,7 +1284,7 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     };
     /* multiples of 4 waves only: a workgroup's waves are dealt to the CU's 4 SIMDs, and 10 waves (640
        lanes) left SIMDs unevenly loaded (box200: 149.6 ms against 123.8 ms at 256, profiles/r03/s3) */
-    const int blocks_all[] = {256, 512, 1024};
+    const int blocks_all[] = {256, 512, 768, 1024};
     auto best = [&](bool rects, int &bb, int &bw) {
         const int bytes = stage_bytes(c, kernel, rects, srcs, nullptr, nullptr);
         bb = p.block;
@@ -1380,6 +1380,14 @@ static int stream_layout(const fmgi_context *c) {
     return smode;
 }
 
+/* the accumulation of a bake's kernel instance: the bucket layout of the stream through per-wave rings
+   (kAccBucket) or through per-workgroup tile lines (kAccLines, FMGI_LINES=1) */
+static int exec_accum(const fmgi_context *c) {
+    if (c->accum != FMGI_ACCUM_STREAM || stream_layout(c) != kStreamBuckets) return c->accum;
+    const char *le = getenv("FMGI_LINES");
+    return (le && atoi(le) == 1) ? kAccLines : kAccBucket;
+}
+
 static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
                        void *events, int32_t *counts, uint32_t *rngf) {
     if (!c || !lm) return set_err(FMGI_ERR_ARG, "fmgi_bake_items: bad arguments");
@@ -1390,7 +1398,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_HYBRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     const bool was_auto = kernel == FMGI_KERNEL_AUTO;
     /* the kernel instance's accumulation: the bucket layout of the stream has its own (kAccBucket) */
-    const int kacc = (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamBuckets) ? kAccBucket : c->accum;
+    const int kacc = exec_accum(c);
     if (was_auto) kernel = c->auto_kernel;
     kernel = fitting_kernel(c, kernel, c->accum, bake_block()); /* an image too large for LDS: same results, other scan */
     if (b == e) return FMGI_OK;

@@ -183,6 +183,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
    stream layouts), kAccBucket = AccBucket (the stream in the per-tile bucket layout, BakeArgs::presort 2:
    its own kernel instance) */
 constexpr int kAccBucket = 5;
+constexpr int kAccLines = 6; /* the bucket layout through per-workgroup tile lines (AccLines) */
 /* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
    FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */
 #define FMGI_KVAR_AXES 0x100

@@ -953,6 +953,9 @@ template <int Mode>
 struct AccStreamT {
     static __device__ __forceinline__ int layout(const BakeArgs &a) { return Mode >= 0 ? Mode : uni(a.presort); }
     static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
+    static __device__ __forceinline__ void init(const BakeArgs &a, uint32_t *ring) {
+        if (layout(a) == 2) bucket_init(a, ring);
+    }
 
     /* a fresh global block for the wave (every live lane learns it) */
     static __device__ __forceinline__ void reserve(const BakeArgs &a, WaveStream &ws) {
@@ -1324,6 +1327,163 @@ struct AccStreamT {
 using AccStream = AccStreamT<-1>; /* unsorted codes / presorted segments (BakeArgs::presort 0, 1) */
 using AccBucket = AccStreamT<2>;  /* per-tile buckets (BakeArgs::presort 2) */
 
+/*
+ * The bucket layout written through per-workgroup tile lines (kAccLines). The per-wave rings cost 6 KB of
+ * LDS per wave and a register-hungry flush (each lane holds 16 codes while the ring is sorted), which held
+ * the bake to 4 waves/SIMD; tracing alone runs 64 ms at 4 waves and 49 ms at 6 (profiles/r04/s3). Here the
+ * workgroup's waves share, per fold tile, a small ring of 16-code lines in LDS (FMGI_LINES_PER_TILE lines):
+ *   - a depositing lane reserves the next position of its tile (one LDS atomic), waits until the line
+ *     slot holding that position is free (the line FMGI_LINES_PER_TILE back has been written out), stores
+ *     its code and counts it into the slot's write counter;
+ *   - the lane whose count completes a line (16 codes) writes the line to the tile's bucket in HBM as one
+ *     64-B run (4 x 16 B) and frees the slot. The workgroup's lines of a tile fill one pool block after
+ *     another (FMGI_BUCKET_BLOCK codes = 64 lines; the lane that takes a block's first line allocates it
+ *     with one atomic on the pool cursor and publishes it, tagged with its sequence number, to the lanes of
+ *     the other lines of that block);
+ *   - after the bake loop (a workgroup barrier), one lane per tile pads its partial line with sentinels,
+ *     writes it and records the length of the tile's last block.
+ * The blocks are the bucket layout k_bucket_fold reads (blocks listed by tile, runs of codes, sentinels
+ * skipped), so the fold is unchanged. Progress: a lane waits only for an older line of its tile, and the
+ * oldest unwritten line of a tile waits for nothing, so it completes; every wave spends the wait storing
+ * the codes of its other lanes. LDS per workgroup: FMGI_LINES_TILES tiles x (68-dword line ring, padded
+ * against bank conflicts across tiles, + counters), 21 KB, against 6 KB per wave for the rings.
+ */
+#define FMGI_LINES_TILES 64        /* tile slots (bucket layouts have P <= 63 tiles)                 */
+#ifndef FMGI_LINES_PER_TILE
+#define FMGI_LINES_PER_TILE 4      /* 16-code lines per tile ring (a power of 2)                     */
+#endif
+#define FMGI_LINES_STRIDE (16 * FMGI_LINES_PER_TILE + 4) /* dwords per tile ring (+4: bank spread across tiles) */
+#define FMGI_LINES_BLKSLOTS 8      /* published block ids per tile ({sequence, id}; a slot is reused 8 blocks later) */
+#define FMGI_LINES_DWORDS (FMGI_LINES_TILES * (FMGI_LINES_STRIDE + 2 + 2 * FMGI_LINES_PER_TILE + 2 * FMGI_LINES_BLKSLOTS))
+#define FMGI_LINES_SPIN (1u << 20) /* bound of every wait (s_sleep 1 each, ~30 ms): past it the bake sets the
+                                      overflow flag and stops waiting, so the call fails loudly, never hangs */
+struct AccLines {
+    static constexpr uint32_t NL = FMGI_LINES_PER_TILE, T = FMGI_LINES_TILES, BP = FMGI_BUCKET_BLOCK;
+    static constexpr uint32_t kSent = 0xFFFFFFFFu, kNoBlock = 0xFFFFFFFFu;
+    static __device__ __forceinline__ int layout(const BakeArgs &) { return 2; }
+    static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
+    static constexpr uint32_t NB = FMGI_LINES_BLKSLOTS;
+    /* the workgroup's region: [T][68] codes, ctr[T], fill[T], wr[T][NL], fl[T][NL], blk[T][NB] x {tag, id} */
+    static __device__ __forceinline__ uint32_t *codes(uint32_t *base) { return base; }
+    static __device__ __forceinline__ uint32_t *ctr(uint32_t *base) { return base + T * FMGI_LINES_STRIDE; }
+    static __device__ __forceinline__ uint32_t *fillc(uint32_t *base) { return ctr(base) + T; }
+    static __device__ __forceinline__ uint32_t *wr(uint32_t *base) { return fillc(base) + T; }
+    static __device__ __forceinline__ uint32_t *fl(uint32_t *base) { return wr(base) + T * NL; }
+    static __device__ __forceinline__ uint2 *blk(uint32_t *base) { return (uint2 *)(fl(base) + T * NL); }
+
+    static __device__ __forceinline__ void init(const BakeArgs &, uint32_t *base) {
+        for (uint32_t i = threadIdx.x; i < T; i += blockDim.x) {
+            ctr(base)[i] = 0;
+            fillc(base)[i] = 0;
+#pragma unroll
+            for (uint32_t k = 0; k < NL; k++) {
+                wr(base)[i * NL + k] = 0;
+                fl(base)[i * NL + k] = k; /* line k may use slot k first */
+            }
+#pragma unroll
+            for (uint32_t k = 0; k < NB; k++) blk(base)[i * NB + k] = make_uint2(kNoBlock, kNoBlock);
+        }
+        __syncthreads();
+    }
+
+    /* write line L of tile t (16 codes in its slot) to the tile's bucket and free the slot */
+    static __device__ __forceinline__ void write_line(const BakeArgs &a, uint32_t *base, uint32_t t, uint32_t L) {
+        const uint32_t sl = L & (NL - 1);
+        const uint4 *src = (const uint4 *)(codes(base) + t * FMGI_LINES_STRIDE + 16 * sl);
+        const uint4 q0 = src[0], q1 = src[1], q2 = src[2], q3 = src[3];
+        const uint32_t u = __hip_atomic_fetch_add(fillc(base) + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        /* the codes are in registers: line L + NL may take the slot */
+        __hip_atomic_store(fl(base) + t * NL + sl, L + NL, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_WORKGROUP);
+        const uint32_t k = u >> 6, pos = u & 63; /* block k of the workgroup's lines of tile t, line pos in it */
+        uint2 *slot = blk(base) + t * NB + (k & (NB - 1));
+        uint32_t b = kNoBlock;
+        /* The lane of a block's first line allocates it and publishes it; the lanes of its other lines wait
+           for that. The publisher may be a lane of this same wave (two lines of one tile completed by one
+           append), so its step must come first in program order: two sequential ifs with a reconvergence
+           point between them, never an if / else the compiler could lay out waiting branch first. */
+        if (pos == 0) {
+            const unsigned long long nb = atomicAdd(a.pool_cursor, 1ull);
+            b = nb < a.pool_blocks ? (uint32_t)nb : kNoBlock;
+            if (b != kNoBlock) {
+                a.block_tile[b] = t;
+                a.block_len[b] = BP; /* every block but the tile's last is filled; finish() sets the last */
+            }
+            __hip_atomic_store((unsigned long long *)slot, ((unsigned long long)b << 32) | k, __ATOMIC_RELEASE,
+                               __HIP_MEMORY_SCOPE_WORKGROUP);
+        }
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (pos != 0) {
+            unsigned long long v = 0;
+            for (uint32_t spin = 0;; spin++) { /* published by the lane of the block's first line */
+                v = __hip_atomic_load((unsigned long long *)slot, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if ((uint32_t)v == k) break;
+                if (spin >= FMGI_LINES_SPIN) { /* never: fail the call instead of hanging */
+                    atomicAdd(a.overflow, 1ull);
+                    return;
+                }
+                __builtin_amdgcn_s_sleep(1);
+            }
+            b = (uint32_t)(v >> 32);
+        }
+        if (b != kNoBlock) {
+            uint4 *d = (uint4 *)(a.stream + (uint64_t)b * BP + 16 * pos);
+            d[0] = q0, d[1] = q1, d[2] = q2, d[3] = q3;
+        } else { /* pool exhausted (never, by sizing): exact atomics into the lightmap */
+            const uint32_t c[16] = {q0.x, q0.y, q0.z, q0.w, q1.x, q1.y, q1.z, q1.w,
+                                    q2.x, q2.y, q2.z, q2.w, q3.x, q3.y, q3.z, q3.w};
+            for (int e = 0; e < 16; e++) AccBucket::bucket_atomic(a, c[e]);
+        }
+    }
+
+    static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &, uint32_t *base, bool dep,
+                                                  uint32_t code) {
+        if (__ballot(dep) == 0) return;
+        const uint32_t t = code >> (10 + FMGI_TILE_BITS);
+        uint32_t old = 0;
+        if (dep) old = __hip_atomic_fetch_add(ctr(base) + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bool pend = dep;
+        for (uint32_t spin = 0;; spin++) {
+            if (pend && spin >= FMGI_LINES_SPIN) { /* never: fail the call instead of hanging */
+                atomicAdd(a.overflow, 1ull);
+                pend = false;
+            }
+            if (pend) {
+                const uint32_t L = old >> 4, sl = L & (NL - 1);
+                const uint32_t f = __hip_atomic_load(fl(base) + t * NL + sl, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_WORKGROUP);
+                if (f == L) { /* the slot holds line L: store the code and count it */
+                    codes(base)[t * FMGI_LINES_STRIDE + 16 * sl + (old & 15)] = code;
+                    const uint32_t w = __hip_atomic_fetch_add(wr(base) + t * NL + sl, 1u, __ATOMIC_ACQ_REL,
+                                                              __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if ((w & 15) == 15) write_line(a, base, t, L); /* this code completed the line */
+                    pend = false;
+                }
+            }
+            if (__ballot(pend) == 0) break;
+            __builtin_amdgcn_s_sleep(1);
+        }
+    }
+
+    /* after the loop: every wave of the workgroup has stored its codes; one lane per tile writes the partial
+       line (padded with sentinels) and the length of the tile's last block */
+    static __device__ __forceinline__ void finish(const BakeArgs &a, WaveStream &, uint32_t *base) {
+        __syncthreads();
+        for (uint32_t t = threadIdx.x; t < (uint32_t)a.ntiles; t += blockDim.x) {
+            const uint32_t n = ctr(base)[t], r = n & 15;
+            if (r) {
+                const uint32_t L = n >> 4, sl = L & (NL - 1);
+                for (uint32_t k = r; k < 16; k++) codes(base)[t * FMGI_LINES_STRIDE + 16 * sl + k] = kSent;
+                write_line(a, base, t, L);
+            }
+            const uint32_t lines = fillc(base)[t];
+            if (lines & 63) {
+                const uint2 v = blk(base)[t * NB + (((lines - 1) >> 6) & (NB - 1))];
+                if (v.y != kNoBlock) a.block_len[v.y] = (lines & 63) * 16;
+            }
+        }
+    }
+};
+
 template <class Acc>
 struct HasAppend {
     static constexpr bool value = false;
@@ -1332,6 +1492,20 @@ template <int Mode>
 struct HasAppend<AccStreamT<Mode>> {
     static constexpr bool value = true;
 };
+template <>
+struct HasAppend<AccLines> {
+    static constexpr bool value = true;
+};
+/* the LDS region of an appending accumulation: the wave's ring (AccStreamT), the workgroup's tile lines
+   (AccLines) */
+template <class Acc>
+__device__ __forceinline__ uint32_t *acc_region(char *lds, const BakeArgs &a) {
+    return (uint32_t *)(lds + a.ring_off) + (threadIdx.x >> 6) * FMGI_RING_STRIDE;
+}
+template <>
+__device__ __forceinline__ uint32_t *acc_region<AccLines>(char *lds, const BakeArgs &a) {
+    return (uint32_t *)(lds + a.ring_off);
+}
 
 /* ---- the per-lane photon state machine ------------------------------------------------------- */
 
@@ -1394,21 +1568,27 @@ __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
  */
 #ifdef FMGI_WAVES_PER_EU /* experiment builds: ask the register allocator for this occupancy */
 #define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(FMGI_WAVES_PER_EU)))
-#else /* ScanGrid: 4 waves/SIMD (108 VGPRs, no spills): with the walls staged, LDS holds a CU to 16 waves anyway */
-#define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(Scan::kMinWaves)))
+#else /* ScanGrid: 4 waves/SIMD (108 VGPRs, no spills): with the walls staged, LDS holds a CU to 16 waves anyway;
+         AccLines leaves the LDS for 6 (768-lane workgroups, two per CU) and asks for the registers of 6 */
+#define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(acc_min_waves<Acc>() > Scan::kMinWaves ? acc_min_waves<Acc>() : Scan::kMinWaves)))
 #endif
+template <class Acc>
+constexpr int acc_min_waves() { return 1; }
+template <>
+constexpr int acc_min_waves<AccLines>() { return 6; }
 template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
-    /* AccStream: this wave's ring of deposit codes, after the scan image in LDS */
-    uint32_t *const ring = (uint32_t *)(s_img + a.ring_off) + (threadIdx.x >> 6) * FMGI_RING_STRIDE;
+    /* AccStream: this wave's ring of deposit codes, after the scan image in LDS (AccLines: the workgroup's
+       tile lines) */
+    uint32_t *const ring = acc_region<Acc>(s_img, a);
     if (Scan::kLds) { /* stage the filter image once per workgroup */
         const int n16 = a.fimg_bytes >> 4;
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
         __syncthreads();
     }
     if constexpr (HasAppend<Acc>::value)
-        if (Acc::layout(a) == 2) Acc::bucket_init(a, ring);
+        Acc::init(a, ring);
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
@@ -1773,6 +1953,7 @@ const void *kernel_acc(int accum, bool trace) {
     if (accum == 3) return kernel_ptr<Scan, AccNone>(trace);
     if (accum == 4) return kernel_ptr<Scan, AccStream>(trace);
     if (accum == kAccBucket) return kernel_ptr<Scan, AccBucket>(trace);
+    if (accum == kAccLines) return kernel_ptr<Scan, AccLines>(trace);
     return kernel_ptr<Scan, AccFx3>(trace);
 }
 
@@ -1782,12 +1963,15 @@ void launch_acc(const BakeArgs &a, int accum, bool trace, dim3 grid, dim3 block,
     else if (accum == 3) launch3<Scan, AccNone>(a, trace, grid, block, lds, s);
     else if (accum == 4) launch3<Scan, AccStream>(a, trace, grid, block, lds, s);
     else if (accum == kAccBucket) launch3<Scan, AccBucket>(a, trace, grid, block, lds, s);
+    else if (accum == kAccLines) launch3<Scan, AccLines>(a, trace, grid, block, lds, s);
     else launch3<Scan, AccFx3>(a, trace, grid, block, lds, s);
 }
 
 const void *bake_kernel(int kernel, int accum, bool trace) {
     if (kernel == FMGI_KERNEL_FAST_COOP)
-        return accum == kAccBucket ? kernel_ptr<ScanFastCoop, AccBucket>(false) : kernel_ptr<ScanFastCoop, AccStream>(false);
+        return accum == kAccBucket ? kernel_ptr<ScanFastCoop, AccBucket>(false)
+                                   : (accum == kAccLines ? kernel_ptr<ScanFastCoop, AccLines>(false)
+                                                         : kernel_ptr<ScanFastCoop, AccStream>(false));
     if (kernel == (2 | FMGI_KVAR_AXES)) return kernel_acc<ScanGridAxes>(accum, trace);
     if (kernel == (4 | FMGI_KVAR_PLAN)) return kernel_acc<ScanHybridPlan>(accum, trace);
     kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN);
@@ -1806,6 +1990,7 @@ int fmgi_kernels_filter_pk() { return FMGI_FILTER_PK; }
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
+    if (accum == kAccLines) return img + (size_t)FMGI_LINES_DWORDS * 4;
     return img + ((accum == 4 || accum == kAccBucket) ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
 
@@ -1846,8 +2031,9 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         if (e != hipSuccess) return e;
     }
     if (kernel == FMGI_KERNEL_FAST_COOP) {
-        if ((accum != 4 && accum != kAccBucket) || trace) return hipErrorInvalidValue; /* stream accumulation only */
+        if ((accum != 4 && accum != kAccBucket && accum != kAccLines) || trace) return hipErrorInvalidValue;
         if (accum == kAccBucket) launch3<ScanFastCoop, AccBucket>(a, false, grid, blk, lds, s);
+        else if (accum == kAccLines) launch3<ScanFastCoop, AccLines>(a, false, grid, blk, lds, s);
         else launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
     } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */
         launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);

@@ -41,9 +41,9 @@ python -c "import __graft_entry__ as g; g.build()" || exit 3
 export TMPDIR=/tmp
 for s in ${FMGI_STEPS:-tests ref bench prof}; do
   case $s in
-    tests) step tests 900 python -m pytest tests -m gpu -q -x -p no:cacheprovider ;;
+    tests) step tests 1100 python -u -m pytest tests -m gpu -v -x -p no:cacheprovider --timeout 900 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
-    tests_k) step tests_k 900 python -m pytest -m gpu -q -x -p no:cacheprovider ${TESTS_ARGS:-tests} ;;
+    tests_k) step tests_k 900 python -u -m pytest -m gpu -v -x -p no:cacheprovider --timeout 120 --timeout-method thread ${TESTS_ARGS:-tests} ;;
     rad)   step rad 900 python tools/bench_rad.py ${RAD_ARGS:-} ;;
     radprof) step radprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/radprof" -o run --output-format csv -- python tools/bench_rad.py --reps 1 --no-cpu-baseline ${RAD_ARGS:-} ;;
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;
