@@ -1284,7 +1284,9 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     };
     /* multiples of 4 waves only: a workgroup's waves are dealt to the CU's 4 SIMDs, and 10 waves (640
        lanes) left SIMDs unevenly loaded (box200: 149.6 ms against 123.8 ms at 256, profiles/r03/s3) */
-    const int blocks_all[] = {256, 512, 768, 1024};
+    /* (768-lane workgroups measured pathological for every instance built for 4 waves/SIMD: box200 bake
+       1.6-2.2 s instead of 0.05-0.08 s, profiles/r04/s7; not offered) */
+    const int blocks_all[] = {256, 512, 1024};
     auto best = [&](bool rects, int &bb, int &bw) {
         const int bytes = stage_bytes(c, kernel, rects, srcs, nullptr, nullptr);
         bb = p.block;
