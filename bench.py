@@ -159,7 +159,7 @@ def cpu_baseline_radiosity(target_s=10.0, procs=1):
     if not os.path.exists(exe):
         return None
     sc = S.box_scene(200, tile_size=2.0, with_light=True)
-    rays = 10_000 * int(sum(int(w["lightmapSetup"][1]) * int(w["lightmapSetup"][2]) for w in sc.walls))
+    rays = 10_000 * int(sum(int(w["lm"][1]) * int(w["lm"][2]) for w in sc.walls))
     with tempfile.TemporaryDirectory() as d:
         g = os.path.join(d, "geometry.bin")
         S.save_geometry(sc, g)
