@@ -257,13 +257,43 @@ struct GridBuild {
     std::vector<int32_t> idx;
 };
 
+/* The quantized inline records of a grid cell (GridCell): the kernel's float ops, replayed in float32 on the
+   host (this file is built without FMA contraction). A record passes the float test iff
+   |fl(x - c)| <= hw; fl(x - c) is monotone in x, so the passing floats form an interval whose ends are
+   found by stepping one ulp at a time from c -/+ hw. */
+static bool grid_pass(float x, float c, float hw) {
+    const float d = x - c;
+    return fabsf(d) <= hw;
+}
+static float grid_end(float c, float hw, bool hi) {
+    float x = hi ? c + hw : c - hw;
+    const float out = hi ? INFINITY : -INFINITY, in = hi ? -INFINITY : INFINITY;
+    for (int k = 0; k < 64 && grid_pass(x, c, hw); k++) x = nextafterf(x, out); /* step out of the interval */
+    for (int k = 0; k < 128 && !grid_pass(x, c, hw); k++) x = nextafterf(x, in); /* back to its last float */
+    return x;
+}
+/* q of float coordinate x in cell column `cell` of an axis with origin o and inverse cell size inv: the
+   kernel's (x - o) * inv, minus the cell, times 2^16, clamped to [0, 65535] and truncated (grid_cell) */
+static uint32_t grid_q(float x, float o, float inv, int cell) {
+    const float d = x - o;
+    const float t = d * inv;
+    const float r = t - (float)cell;
+    const float m = r * 65536.0f;
+    return (uint32_t)std::min(std::max(m, 0.0f), 65535.0f);
+}
+static uint32_t grid_bounds(float c, float hw, float o, float inv, int cell) {
+    const float a = grid_end(c, hw, false), b = grid_end(c, hw, true);
+    if (!grid_pass(a, c, hw) || !grid_pass(b, c, hw)) return 0xFFFF0000u; /* (a degenerate record) pass-all */
+    return grid_q(a, o, inv, cell) | (grid_q(b, o, inv, cell) << 16);
+}
+
 GridBuild build_grid(const FilterBuild &fb) {
     GridBuild gb;
     /* cells per record the cost model may spend (FMGI_GRID_CPR, experiments: coarser grids are smaller) */
     int cells_per_record = 16;
     if (const char *ce = getenv("FMGI_GRID_CPR"))
         if (atoi(ce) >= 1 && atoi(ce) <= 64) cells_per_record = atoi(ce);
-    gb.cells.push_back(GridCell{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0, -1, -1, 0}); /* cell 0: empty */
+    gb.cells.push_back(GridCell{kGridNoRec, kGridNoRec, kGridNoRec, kGridNoRec, 0, -1, -1, 0}); /* cell 0: empty */
     std::vector<GridPlane> planes[3][2];
     for (int a = 0; a < 3; a++) {
         for (int c = 0; c < 2; c++) {
@@ -368,15 +398,19 @@ GridBuild build_grid(const FilterBuild &fb) {
                     for (int iv = v0; iv <= v1; iv++)
                         for (int iu = u0; iu <= u1; iu++) bucket[(size_t)iv * nu + iu].push_back(r);
                 }
-                for (const auto &b : bucket) {
-                    GridCell gc{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, (int32_t)b.size(), -1, -1,
+                for (size_t ci = 0; ci < bucket.size(); ci++) {
+                    const auto &b = bucket[ci];
+                    const int iu = (int)(ci % (size_t)nu), iv = (int)(ci / (size_t)nu);
+                    GridCell gc{kGridNoRec, kGridNoRec, kGridNoRec, kGridNoRec, (int32_t)b.size(), -1, -1,
                                 (int32_t)gb.idx.size()};
                     if (b.size() > 0) {
-                        gc.cu0 = b[0]->cu, gc.hwu0 = b[0]->hwu, gc.cv0 = b[0]->cv, gc.hwv0 = b[0]->hwv;
+                        gc.qu0 = grid_bounds(b[0]->cu, b[0]->hwu, g.u0, g.iu, iu);
+                        gc.qv0 = grid_bounds(b[0]->cv, b[0]->hwv, g.v0, g.iv, iv);
                         gc.idx0 = b[0]->idx;
                     }
                     if (b.size() > 1) {
-                        gc.cu1 = b[1]->cu, gc.hwu1 = b[1]->hwu, gc.cv1 = b[1]->cv, gc.hwv1 = b[1]->hwv;
+                        gc.qu1 = grid_bounds(b[1]->cu, b[1]->hwu, g.u0, g.iu, iu);
+                        gc.qv1 = grid_bounds(b[1]->cv, b[1]->hwv, g.v0, g.iv, iv);
                         gc.idx1 = b[1]->idx;
                     }
                     for (size_t k = 2; k < b.size(); k++) {
@@ -965,8 +999,8 @@ static const size_t kBakeLdsMax = 160 * 1024;
 /* whether a hybrid bake reads the full image (the floor-plan walk, FMGI_PLAN=1, or the one-record wall loop
    of FMGI_FILTER_PK=0 builds) rather than the default one (plane image + wall pairs only) */
 static bool hybrid_full(const fmgi_context *c) {
-    const char *pe = getenv("FMGI_PLAN");
-    return !fmgi_kernels_filter_pk() || (c->plan_off >= 0 && pe && atoi(pe) == 1);
+    const char *pe = getenv("FMGI_PLAN"), *fe = getenv("FMGI_HYB_FULL"); /* FMGI_HYB_FULL=1: A/B of the image */
+    return !fmgi_kernels_filter_pk() || (c->plan_off >= 0 && pe && atoi(pe) == 1) || (fe && atoi(fe) == 1);
 }
 
 static int image_bytes(const fmgi_context *c, int kernel) {

@@ -45,16 +45,19 @@ struct GridPlane {
 };
 static_assert(sizeof(GridPlane) == 64, "GridPlane must be 64 B");
 
-/* One grid cell (48 B): its first two records inline {cu, hwu, cv, hwv} with their rect indices, so a
-   lookup in a cell of <= 2 records is one load and needs no index load; records 3..count live in the
-   overflow arrays at [rest, rest + count - 2). An absent inline record is {0, -1, 0, -1} (never a
-   candidate). */
+/* One grid cell (32 B: two 16-B loads per lookup). Its first two records are inline as quantized bounds
+   with their rect indices; records 3..count live in the overflow arrays at [rest, rest + count - 2) as
+   float records. The kernel maps a hit point to the cell's 16-bit fixed-point coordinates
+   q = clamp(floor((t - cell) * 65536), 0, 65535), t its float cell coordinate (grid_cell); a record's
+   bounds {lo | hi << 16} per axis are q at the smallest and largest float that pass the record's float
+   test |x - c| <= hw, so every point that passes the float test passes lo <= q <= hi (q is monotone in x):
+   a superset, as the exactness argument needs. An absent record is {0xFFFF, 0} (never a candidate). */
 struct GridCell {
-    float cu0, hwu0, cv0, hwv0;
-    float cu1, hwu1, cv1, hwv1;
+    uint32_t qu0, qv0, qu1, qv1;
     int32_t count, idx0, idx1, rest;
 };
-static_assert(sizeof(GridCell) == 48, "GridCell must be 48 B");
+static_assert(sizeof(GridCell) == 32, "GridCell must be 32 B");
+constexpr uint32_t kGridNoRec = 0xFFFFu; /* lo 0xFFFF, hi 0: no q passes */
 
 struct BakeArgs {
     const RectDev *rects;

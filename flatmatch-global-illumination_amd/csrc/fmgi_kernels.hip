@@ -399,14 +399,20 @@ using ScanFastCoop = ScanFastT<true>;
  * its separation argument carry over unchanged. A closed box of 200 rects has 6 planes: ~3 cells and a
  * few records per scan instead of ~100 rect tests.
  */
-/* The kernel's cell of hit point (uh, vh) on plane record g (64 B, see GridPlane). */
-__device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, const float4 g2, float uh, float vh) {
+/* The kernel's cell of hit point (uh, vh) on plane record g (64 B, see GridPlane), and the point's
+   16-bit fixed-point coordinates (qu, qv) inside that cell, against which the cell's inline records are
+   tested (GridCell; the host derives their bounds from these same float ops, fmgi_api.cpp grid_q). */
+__device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, const float4 g2, float uh, float vh,
+                                              uint32_t &qu, uint32_t &qv) {
     /* g0 = {plane, u0, v0, iu}, g1 = {iv, mu, mv, nu}, g2 = {nv, cell_off, -, -} */
     /* clamp to [0, n - 1]: v_med3_f32 (fminf(fmaxf()) adds a canonicalising max); the same cell for
-       every non-NaN coordinate, and a NaN hit point passes no record test in any cell */
-    const float tu = __builtin_amdgcn_fmed3f((uh - g0.y) * g0.w, 0.0f, g1.y);
-    const float tv = __builtin_amdgcn_fmed3f((vh - g0.z) * g1.x, 0.0f, g1.z);
-    return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)tv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)tu;
+       every non-NaN coordinate */
+    const float ru = (uh - g0.y) * g0.w, rv = (vh - g0.z) * g1.x;
+    const float cu = __builtin_floorf(__builtin_amdgcn_fmed3f(ru, 0.0f, g1.y));
+    const float cv = __builtin_floorf(__builtin_amdgcn_fmed3f(rv, 0.0f, g1.z));
+    qu = (uint32_t)__builtin_amdgcn_fmed3f((ru - cu) * 65536.0f, 0.0f, 65535.0f);
+    qv = (uint32_t)__builtin_amdgcn_fmed3f((rv - cv) * 65536.0f, 0.0f, 65535.0f);
+    return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)cv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)cu;
 }
 
 /* the grid cells, in global memory (L2-resident). Always a global pointer: a pointer that may point into
@@ -427,13 +433,27 @@ __device__ __forceinline__ void grid_rec(float f, float uh, float vh, float4 r, 
     L1 = lt ? key : L1;
 }
 
-/* the candidate tests of one cell: its two inline records (absent ones are never candidates), then its
-   overflow records (rare); code1 receives the winner's rect index */
+/* one inline record of a cell against the point's fixed-point cell coordinates: {lo | hi << 16} per axis */
+__device__ __forceinline__ bool grid_qpass(uint32_t qu, uint32_t qv, uint32_t bu, uint32_t bv) {
+    return (int)(qu >= (bu & 0xFFFFu)) & (int)(qu <= (bu >> 16)) & (int)(qv >= (bv & 0xFFFFu)) & (int)(qv <= (bv >> 16));
+}
+__device__ __forceinline__ void grid_recq(float f, uint32_t qu, uint32_t qv, uint32_t bu, uint32_t bv, int code,
+                                          float &L1, float &L2, int &code1) {
+    const float key = grid_qpass(qu, qv, bu, bv) ? f : INFINITY;
+    const bool lt = key < L1;
+    L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+    code1 = lt ? code : code1;
+    L1 = lt ? key : L1;
+}
+
+/* the candidate tests of one cell: its two inline records (quantized bounds; absent ones are never
+   candidates), then its overflow records (float, rare); code1 receives the winner's rect index */
 __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const GridCell &c, float f, float uh, float vh,
-                                                float &L1, float &L2, int &code1, unsigned &ntest) {
+                                                uint32_t qu, uint32_t qv, float &L1, float &L2, int &code1,
+                                                unsigned &ntest) {
     ntest += (unsigned)c.count;
-    grid_rec(f, uh, vh, make_float4(c.cu0, c.hwu0, c.cv0, c.hwv0), c.idx0 | a.grid_code_or, L1, L2, code1);
-    grid_rec(f, uh, vh, make_float4(c.cu1, c.hwu1, c.cv1, c.hwv1), c.idx1 | a.grid_code_or, L1, L2, code1);
+    grid_recq(f, qu, qv, c.qu0, c.qv0, c.idx0 | a.grid_code_or, L1, L2, code1);
+    grid_recq(f, qu, qv, c.qu1, c.qv1, c.idx1 | a.grid_code_or, L1, L2, code1);
     if (c.count > 2) {
         const float4 *recs = (const float4 *)a.grecs;
         for (int k = 2; k < c.count; k++)
@@ -477,7 +497,9 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *lds, in
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         const float4 g2 = p[8 * j + 2], g3 = p[8 * j + 3];
         if (uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y) continue;
-        grid_cell_tests(a, cells[grid_cell(g0, p[8 * j + 1], g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
+        uint32_t qu, qv;
+        const uint32_t ci = grid_cell(g0, p[8 * j + 1], g2, uh, vh, qu, qv);
+        grid_cell_tests(a, cells[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
 }
 
@@ -521,8 +543,11 @@ __device__ __forceinline__ void grid_xy_merged(const BakeArgs &a, const char *ld
         const float4 *p = ux ? px + 8 * jx : py + 8 * jy;
         const float uh = fmaf(ux ? d.y : d.x, f, ux ? s.y : s.x), vh = fmaf(d.z, f, s.z);
         const float4 g2 = p[2], g3 = p[3];
-        if (!(uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y))
-            grid_cell_tests(a, cells[grid_cell(p[0], p[1], g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
+        if (!(uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y)) {
+            uint32_t qu, qv;
+            const uint32_t ci = grid_cell(p[0], p[1], g2, uh, vh, qu, qv);
+            grid_cell_tests(a, cells[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        }
         if (ux) {
             jx++;
             fx = grid_plane_fac(px, jx, Jx, s.x, rx);
@@ -585,7 +610,9 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * q + (da < 0.0f ? 0 : 64), 16);
         const float4 g0 = p[0], g1 = p[1], g2 = p[2];
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        grid_cell_tests(a, cells[grid_cell(g0, g1, g2, uh, vh)], f, uh, vh, L1, L2, code1, ntest);
+        uint32_t qu, qv;
+        const uint32_t ci = grid_cell(g0, g1, g2, uh, vh, qu, qv);
+        grid_cell_tests(a, cells[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
 }
 
@@ -606,8 +633,9 @@ __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *i
     constexpr int V = (A == 2) ? 1 : 2;
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * A + (comp<A>(d) < 0.0f ? 0 : 64), 16);
     const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
-    grid_cell_tests(a, (grid_cells(a, img))[grid_cell(p[0], p[1], p[2], uh, vh)], f, uh, vh, L1, L2, code1,
-                    ntest);
+    uint32_t qu, qv;
+    const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
+    grid_cell_tests(a, (grid_cells(a, img))[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
 }
 
 __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
@@ -630,8 +658,9 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
         const float du = (m == 0) ? d.y : d.x, dv = mz ? d.y : d.z;
         const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * m + (dm < 0.0f ? 0 : 64), 16);
         const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
-        grid_cell_tests(a, (grid_cells(a, img))[grid_cell(p[0], p[1], p[2], uh, vh)], fm, uh, vh, L1, L2,
-                        code1, ntest);
+        uint32_t qu, qv;
+        const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
+        grid_cell_tests(a, (grid_cells(a, img))[ci], fm, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
     const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
     if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0>(a, img, s, d, fx, L1, L2, code1, ntest);
@@ -656,9 +685,10 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
         const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        const GridCell c = cells[grid_cell(g0, g1, g2, uh, vh)];
-        if (c.count > 0 && (int)(fabsf(uh - c.cu0) <= c.hwu0) & (int)(fabsf(vh - c.cv0) <= c.hwv0)) fn(c.idx0);
-        if (c.count > 1 && (int)(fabsf(uh - c.cu1) <= c.hwu1) & (int)(fabsf(vh - c.cv1) <= c.hwv1)) fn(c.idx1);
+        uint32_t qu, qv;
+        const GridCell c = cells[grid_cell(g0, g1, g2, uh, vh, qu, qv)];
+        if (c.count > 0 && grid_qpass(qu, qv, c.qu0, c.qv0)) fn(c.idx0);
+        if (c.count > 1 && grid_qpass(qu, qv, c.qu1, c.qv1)) fn(c.idx1);
         for (int k = 2; k < c.count; k++) {
             const float4 r = recs[c.rest + k - 2];
             if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[c.rest + k - 2]);

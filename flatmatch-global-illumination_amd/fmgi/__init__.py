@@ -271,9 +271,9 @@ GRID_PLANE_DTYPE = np.dtype([("plane", "<f4"), ("u0", "<f4"), ("v0", "<f4"), ("i
                              ("ulo", "<f4"), ("uhi", "<f4"), ("vlo", "<f4"), ("vhi", "<f4"),
                              ("pad0", "<f4"), ("pad1", "<f4")])
 assert GRID_PLANE_DTYPE.itemsize == 64
-GRID_CELL_DTYPE = np.dtype([("r0", "<f4", (4,)), ("r1", "<f4", (4,)), ("count", "<i4"), ("idx0", "<i4"),
+GRID_CELL_DTYPE = np.dtype([("q0", "<u4", (2,)), ("q1", "<u4", (2,)), ("count", "<i4"), ("idx0", "<i4"),
                             ("idx1", "<i4"), ("rest", "<i4")])
-assert GRID_CELL_DTYPE.itemsize == 48
+assert GRID_CELL_DTYPE.itemsize == 32
 
 
 def make_geometry(sc: Scene, texels: np.ndarray):

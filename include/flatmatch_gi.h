@@ -271,9 +271,10 @@ int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, 
        -n class}, each {float plane, u0, v0, iu, iv, mu, mv; int32 nu, nv, cell_off; float ulo, uhi,
        vlo, vhi (the records' box, rounded outward), pad[2]} (64 B; mu = nu - 1, mv = nv - 1; NaN
        plane = padding);
-     cells[sizes[3]] (48 B each): the cell's first two records {float cu, hwu, cv, hwv} (margin-grown
-       extents; {0, -1, 0, -1} when absent), then {int32 count, rect index of record 0, of record 1,
-       first overflow entry};
+     cells[sizes[3]] (32 B each): the cell's first two records as quantized bounds {uint32 qu, qv} each
+       ({lo | hi << 16} of the cell's 16-bit fixed-point coordinates that the record's margin-grown
+       extent can reach; {0xFFFF, 0xFFFF} when absent), then {int32 count, rect index of record 0, of
+       record 1, first overflow entry};
      recs[4 * sizes[4]], idx[sizes[4]]: the overflow records (entries 3..count of every cell) and their
        rect indices. */
 int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);

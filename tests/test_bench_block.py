@@ -62,3 +62,14 @@ def test_valu_ceiling_summary_is_committed_and_consistent():
     assert by[1] < by[2] <= max(by.values()) <= d["spec_fma_per_simd_cycle"] == pytest.approx(0.5, rel=0.01)
     for w, c in d["counters"]["fma64"].items():
         assert c["valu_per_simd_cycle"] == pytest.approx(by[int(w)], rel=0.05), (w, c)
+
+
+@pytest.mark.skipif(not os.path.exists(os.path.join(REPO, "oracle", "_ref", "rad_ref")),
+                    reason="oracle/_ref not built (needs /root/reference at build time)")
+def test_radiosity_cpu_leg_runs():
+    """bench.py's cpu_baseline_radiosity: the reference's performRadiosityNative on the lit 2-m-tile box,
+    labelled not photon-comparable (north_star: radiosityNative.c timed on the host cores in the same run)."""
+    b = _bench()
+    r = b.cpu_baseline_radiosity(procs=1)
+    assert r["kind"] == "reference" and r["comparable"] is False and r["cores"] == 1
+    assert r["unit"] == "form-factor rays/s" and r["value"] > 0

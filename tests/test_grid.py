@@ -4,7 +4,9 @@ ScanGrid (csrc/fmgi_kernels.hip) is exact only if, for every hit point (u, v) on
 cell the kernel computes for (u, v) lists EVERY record of that plane whose margin-grown extent
 contains (u, v) -- the candidate set must stay a superset of photonmap.cl's valid set V. Here the
 kernel's cell arithmetic is replayed in float32 (IEEE, same operation order) on random points and on
-adversarial points at every record's extent boundaries (and one ulp either side)."""
+adversarial points at every record's extent boundaries (and one ulp either side). A cell holds its first
+two records as quantized bounds of the cell's 16-bit fixed-point coordinates (GridCell): every point that
+passes a record's float test must also pass its quantized test, replayed the same way."""
 import numpy as np
 import pytest
 
@@ -15,7 +17,11 @@ def _tables(sc):
     ctx = fmgi.Context(-1)
     ctx.set_scene(sc)
     t = ctx.grid_tables()
+    f = ctx.filter_image()["recs"]
     ctx.close()
+    # every rect's float record {cu, hwu, cv, hwv} (the filter image holds each axis-aligned rect once)
+    ids = f[:, 5].copy().view(np.int32)
+    t["rec_of"] = {int(i): f[k, 1:5].astype(np.float32) for k, i in enumerate(ids) if i >= 0}
     return t
 
 
@@ -40,11 +46,23 @@ def _cell_of(p, u, v):
     return tv.astype(np.int64) * int(p["nu"]) + tu.astype(np.int64)
 
 
+def _q(p, u, v):
+    """The kernel's 16-bit fixed-point coordinates of (u, v) inside its cell (grid_cell)."""
+    f32 = np.float32
+    out = []
+    for x, o, inv, m in ((u, p["u0"], p["iu"], p["mu"]), (v, p["v0"], p["iv"], p["mv"])):
+        r = (x - f32(o)) * f32(inv)
+        c = np.floor(np.minimum(np.maximum(r, f32(0)), f32(m)))
+        q = np.minimum(np.maximum((r - c) * f32(65536), f32(0)), f32(65535))
+        out.append(q.astype(np.uint32))
+    return out
+
+
 def _entries(t, c):
-    """(records [n, 4], rect indices [n]) of one cell: the inline first record, then the overflow."""
+    """(records [n, 4], rect indices [n]) of one cell: the inline first two, then the overflow."""
     n = int(c["count"])
-    inline = np.array([c["r0"], c["r1"]], np.float32)[: min(n, 2)]
     ids = np.array([c["idx0"], c["idx1"]], np.int32)[: min(n, 2)]
+    inline = np.array([t["rec_of"][int(i)] for i in ids], np.float32).reshape(-1, 4)
     rest = slice(int(c["rest"]), int(c["rest"]) + max(n - 2, 0))
     return np.concatenate([inline, t["recs"][rest]]), np.concatenate([ids, t["idx"][rest]]).astype(np.int32)
 
@@ -88,6 +106,22 @@ def _check_plane(t, p, cells, rng):
         if not need <= lists[cell[k]]:
             missing += 1
     assert missing == 0, f"{missing} points whose containing records are not in their cell"
+    # the cell's inline records: every point that passes a record's float test passes its quantized bounds
+    qu, qv = _q(p, U, V)
+    col = {int(i): k for k, i in enumerate(ids)}
+    bad = 0
+    for slot, qname in ((0, "q0"), (1, "q1")):
+        ce = cells[cell]
+        has = ce["count"] > slot
+        rid = ce["idx0"] if slot == 0 else ce["idx1"]
+        b = ce[qname]
+        for k in np.nonzero(has)[0]:
+            j = col[int(rid[k])]
+            if inside[k, j]:
+                bu, bv = int(b[k, 0]), int(b[k, 1])
+                ok = (bu & 0xFFFF) <= qu[k] <= (bu >> 16) and (bv & 0xFFFF) <= qv[k] <= (bv >> 16)
+                bad += not ok
+    assert bad == 0, f"{bad} points pass a record's float test but not its quantized bounds"
     # the plane's cull box (grid_axis skips the cell when the hit point is outside it): no point outside
     # the box passes any record's float test |x - c| <= hw, so skipping cannot drop a candidate
     f32 = np.float32
