@@ -318,7 +318,16 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
         if (t[k] != 0xFFFFFFFFu) list[base[t[k]] + rk[k]] = (uint32_t)(b0 + (uint64_t)k * kListThreads + threadIdx.x);
 }
 
-__global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict__ pool,
+/* EXP (experiments, FMGI_EXP_FOLD; PROFILING, results wrong): 1 = the codes read and discarded (the
+   read alone), 2 = one LDS add per code and no colour lookup, 3 = the colour lookup and the R add only,
+   4 = the three adds of a colour computed from the code (no lookup). box200, 1e9 photons (profiles/r04/
+   s13-s17): the fold 10.9 ms; 1 = 5.8 ms, 2 = 6.3 ms: the adds, not the reads, bind it. Issuing a quad's
+   four colour reads before its adds (12.2 ms) or adding the tinted differences unconditionally (13.8 ms)
+   was slower. */
+/* 8 waves per SIMD (<= 64 VGPRs): two 1024-lane workgroups per CU, as their 64 KB of LDS allow (at 66
+   VGPRs only one fitted, and the fold took 13.7 ms instead of 11) */
+template <int EXP>
+__global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restrict__ pool,
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ block_len,
                                                      const uint32_t *__restrict__ counts, int P, int G,
@@ -375,7 +384,7 @@ __global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict
        codes are summed */
     const uint32_t span = j_hi - j_lo;
     const uint32_t nb = span > (uint32_t)wave ? (span - (uint32_t)wave + waves - 1) / waves : 0u;
-    const uint4 sent4 = make_uint4(kSentinel, kSentinel, kSentinel, kSentinel);
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     for (uint32_t k0 = 0; k0 < nb; k0 += 64) {
         const uint32_t kn = min(nb - k0, 64u);
         uint32_t lb = 0, ll = 0;
@@ -383,23 +392,25 @@ __global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict
             lb = list[off + j_lo + wave + (k0 + lane) * waves];
             ll = min(block_len[lb], BP);
         }
-        uint4 q[4];
+        u32x4 q[4];
         uint32_t len = 0;
-        auto fetch = [&](uint32_t k, uint4 (&qq)[4], uint32_t &ln) {
+        /* the whole 4-KB block, unconditionally (codes past the block's length are skipped when summed):
+           four 16-B loads per lane with no branch around them, so the wait before a block's sums leaves
+           the next block's loads in flight (loads under a lane condition compiled to 16 dword loads each,
+           and the wait at the branch's join waited for the prefetch too) */
+        auto fetch = [&](uint32_t k, u32x4 (&qq)[4], uint32_t &ln) {
             const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)lb, (int)k);
             ln = (uint32_t)__builtin_amdgcn_readlane((int)ll, (int)k);
-            const uint4 *blk = (const uint4 *)(pool + (uint64_t)b * BP);
+            const __attribute__((address_space(1))) u32x4 *blk =
+                (const __attribute__((address_space(1))) u32x4 *)(pool + (uint64_t)b * BP);
 #pragma unroll
-            for (int u = 0; u < 4; u++) { /* 16-B unit i4 = 64 u + lane: codes 4 i4 .. 4 i4 + 3 */
-                const uint32_t i4 = 64 * u + lane;
-                qq[u] = 4 * i4 < ln ? blk[i4] : sent4;
-            }
+            for (int u = 0; u < 4; u++) qq[u] = blk[64 * u + lane]; /* codes 4 i4 .. 4 i4 + 3, i4 = 64 u + lane */
         };
         fetch(0, q, len);
         for (uint32_t k = 0; k < kn; k++) {
-            uint4 qn[4] = {sent4, sent4, sent4, sent4};
+            u32x4 qn[4];
             uint32_t lenn = 0;
-            if (k + 1 < kn) fetch(k + 1, qn, lenn);
+            fetch(k + 1 < kn ? k + 1 : k, qn, lenn); /* (the last one re-reads this block: unused) */
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t i0 = 4 * (64 * u + lane);
@@ -409,8 +420,18 @@ __global__ __launch_bounds__(1024) void k_bucket_fold(const uint32_t *__restrict
                     const uint32_t c = cs[m];
                     if (i0 + m >= len || c == kSentinel) continue; /* runs are padded to 4 codes */
                     const int tx = (int)((c >> 10) & (kTileTexels - 1));
-                    const uint4 cc = col[c & 1023];
+                    if (EXP == 1) {
+                        if (c == 0x7FFFFFFFu) acc_r[tx] = 1; /* never: keeps the loads */
+                        continue;
+                    }
+                    if (EXP == 2) {
+                        atomicAdd(&acc_r[tx], 1ull);
+                        continue;
+                    }
+                    const uint4 cc = EXP == 4 ? make_uint4(c & 1023, (c & 3) ? c & 511 : 0u, (c & 3) ? c & 255 : 0u, 0u)
+                                              : col[c & 1023];
                     atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
+                    if (EXP == 3) continue;
                     if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
                     if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
                 }
@@ -447,14 +468,22 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                            P, sb.tile_blocks);
         hipLaunchKernelGGL(k_bucket_list, dim3(lg), dim3(kListThreads), 0, s, sb.block_tile, sb.cursor, sb.pool_blocks, P,
                            sb.tile_blocks, sb.tile_blocks + FMGI_PRESORT_MAX_TILES + 1, sb.block_list);
-        e = fmgi_set_lds_attr_once<3>((const void *)k_bucket_fold, (int)plds);
+        const char *xe = getenv("FMGI_EXP_FOLD");
+        const int exp = xe ? atoi(xe) : 0;
+        typedef void (*FoldFn)(const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, int, int, int,
+                               const uint4 *, unsigned long long *, int);
+        static const FoldFn folds[] = {k_bucket_fold<0>, k_bucket_fold<1>, k_bucket_fold<2>, k_bucket_fold<3>,
+                                       k_bucket_fold<4>};
+        const FoldFn fn = folds[exp >= 0 && exp <= 4 ? exp : 0];
+        e = fn == folds[0] ? fmgi_set_lds_attr_once<3>((const void *)fn, (int)plds)
+                           : hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
         const char *be = getenv("FMGI_FOLD_BALANCE"); /* experiments: 0 = equal groups per tile */
         const int balanced = be ? atoi(be) != 0 : 1;
-        hipLaunchKernelGGL(k_bucket_fold, dim3((unsigned)(P * G)), dim3(sb.block > 0 ? sb.block : 1024), plds, s,
-                           sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G, balanced,
-                           (const uint4 *)sb.colpack, lm, num_texels);
+        const dim3 grid((unsigned)(P * G)), blk(sb.block > 0 ? sb.block : 1024);
+        hipLaunchKernelGGL(fn, grid, blk, plds, s, sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G,
+                           balanced, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
     if (sb.presort) {

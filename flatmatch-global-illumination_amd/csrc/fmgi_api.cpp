@@ -1274,16 +1274,20 @@ FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
  */
 struct StagePlan {
     int block = 256;
-    int bytes = 0;                   /* staged blob = image (16-B aligned) | rects | srcs */
-    int rects_off = -1, srcs_off = -1;
+    int bytes = 0;                   /* staged blob = image (16-B aligned) | rects | srcs | cells */
+    int rects_off = -1, srcs_off = -1, cells_off = -1;
 };
 
-static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, int *roff, int *soff) {
+static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, bool cells, int *roff, int *soff,
+                       int *coff = nullptr) {
     int off = (image_bytes(c, kernel) + 15) & ~15;
     if (roff) *roff = rects ? off : -1;
     if (rects) off += c->nrects * (int)sizeof(RectLds);
     if (soff) *soff = srcs ? off : -1;
     if (srcs) off += c->nsrcs * (int)sizeof(SrcDev);
+    off = (off + 15) & ~15;
+    if (coff) *coff = cells ? off : -1;
+    if (cells) off += c->grid_cells * (int)sizeof(GridCell);
     return off;
 }
 
@@ -1321,8 +1325,11 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     /* (768-lane workgroups measured pathological for every instance built for 4 waves/SIMD: box200 bake
        1.6-2.2 s instead of 0.05-0.08 s, profiles/r04/s7; not offered) */
     const int blocks_all[] = {256, 512, 1024};
+    /* the grid cells (experiments, FMGI_CELLS_LDS=1: every cell lookup an LDS read instead of an L2 one) */
+    const char *ce = getenv("FMGI_CELLS_LDS");
+    bool cells = ce && atoi(ce) == 1 && (kernel == FMGI_KERNEL_GRID || kernel == FMGI_KERNEL_HYBRID);
     auto best = [&](bool rects, int &bb, int &bw) {
-        const int bytes = stage_bytes(c, kernel, rects, srcs, nullptr, nullptr);
+        const int bytes = stage_bytes(c, kernel, rects, srcs, cells, nullptr, nullptr);
         bb = p.block;
         bw = waves(p.block, bytes);
         if (forced_block) return;
@@ -1341,8 +1348,13 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
            walls staged 77.6 ms, 20 waves without 123.8 ms), not two */
         rects = rects_mode == 1 ? w1 > 0 : (w1 > 0 && w1 >= std::min(w0, 16));
     }
+    if (cells && (rects ? w1 : w0) <= 0) { /* the cells do not fit beside the rest: not staged */
+        cells = false;
+        best(false, b0, w0);
+        if (rects) best(true, b1, w1);
+    }
     p.block = rects ? b1 : b0;
-    p.bytes = stage_bytes(c, kernel, rects, srcs, &p.rects_off, &p.srcs_off);
+    p.bytes = stage_bytes(c, kernel, rects, srcs, cells, &p.rects_off, &p.srcs_off, &p.cells_off);
     return p;
 }
 
@@ -1502,10 +1514,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.fimg_bytes = c->fimg_bytes;
         for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
     }
-    a.rects_off = a.srcs_off = -1;
-    if (sp.rects_off >= 0 || sp.srcs_off >= 0) { /* the blob: image | RectDev table | SrcDev table */
+    a.rects_off = a.srcs_off = a.cells_off = -1;
+    if (sp.rects_off >= 0 || sp.srcs_off >= 0 || sp.cells_off >= 0) { /* the blob: image | rects | srcs | cells */
         const uint64_t key = (c->scene_gen << 8) | (kernel == FMGI_KERNEL_HYBRID && hybrid_full(c) ? 0x40u : 0u) |
-                             ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) | (sp.srcs_off >= 0 ? 1u : 0u);
+                             ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) | (sp.srcs_off >= 0 ? 1u : 0u) |
+                             (sp.cells_off >= 0 ? 0x80u : 0u);
         if (c->blob_key != key) {
             if (c->blob_cap < (size_t)sp.bytes) {
                 HIPCHK(hipStreamSynchronize(s)); /* no earlier bake may still stage the old blob */
@@ -1539,12 +1552,16 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             if (sp.srcs_off >= 0)
                 HIPCHK(hipMemcpyAsync(c->d_blob + sp.srcs_off, c->d_srcs, (size_t)c->nsrcs * sizeof(SrcDev),
                                       hipMemcpyDeviceToDevice, s));
+            if (sp.cells_off >= 0)
+                HIPCHK(hipMemcpyAsync(c->d_blob + sp.cells_off, c->d_gcells, (size_t)c->grid_cells * sizeof(GridCell),
+                                      hipMemcpyDeviceToDevice, s));
             c->blob_key = key;
         }
         a.fimg = c->d_blob;
         a.fimg_bytes = sp.bytes;
         a.rects_off = sp.rects_off;
         a.srcs_off = sp.srcs_off;
+        a.cells_off = sp.cells_off;
     }
     a.general = c->d_general;
     a.ngeneral = c->ngeneral;

@@ -93,6 +93,7 @@ struct BakeArgs {
     /* >= 0: byte offsets in the staged LDS blob (fimg) of a copy of the RectDev table (the phase-2 reads of
        the scans' winners) and of the SrcDev table (every photon's emission); -1: read from global memory */
     int rects_off, srcs_off;
+    int cells_off;        /* >= 0: byte offset of a copy of the grid cells (GridCell) in the staged blob */
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
     int plan_off;         /* ScanHybridPlan: byte offset of the floor plan in the image (-1: none)      */

@@ -415,11 +415,26 @@ __device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, 
     return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)cv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)cu;
 }
 
-/* the grid cells, in global memory (L2-resident). Always a global pointer: a pointer that may point into
-   LDS or global memory compiles to flat loads, which count in both vmcnt and lgkmcnt and make every
-   LDS wait after them wait for the cell too (staging the cells in LDS was measured at +-0 %) */
-__device__ __forceinline__ const GridCell *grid_cells(const BakeArgs &a, const char *) {
-    return (const GridCell *)a.gcells;
+/* grid cell ci: from the workgroup's LDS copy of the cell table when the host staged it there
+   (BakeArgs::cells_off >= 0), else from global memory (L2-resident). The two reads stay in their own
+   address spaces: a pointer that may point into either compiles to flat loads, which count in both
+   vmcnt and lgkmcnt and make every LDS wait after them wait for the cell too. */
+__device__ __forceinline__ GridCell load_cell(const BakeArgs &a, const char *lds, uint32_t ci) {
+    typedef uint32_t u4 __attribute__((ext_vector_type(4)));
+    u4 q, r;
+    if (uni(a.cells_off) >= 0) {
+        const __attribute__((address_space(3))) u4 *l = (const __attribute__((address_space(3))) u4 *)(
+            (const __attribute__((address_space(3))) char *)lds + a.cells_off);
+        q = l[2 * ci];
+        r = l[2 * ci + 1];
+    } else {
+        q = ((gptr<u4>)a.gcells)[2 * ci];
+        r = ((gptr<u4>)a.gcells)[2 * ci + 1];
+    }
+    GridCell c;
+    c.qu0 = q.x; c.qv0 = q.y; c.qu1 = q.z; c.qv1 = q.w;
+    c.count = (int)r.x; c.idx0 = (int)r.y; c.idx1 = (int)r.z; c.rest = (int)r.w;
+    return c;
 }
 
 /* one candidate test of ScanGrid's phase 1: record r against hit point (uh, vh) at fac' f */
@@ -480,7 +495,6 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *lds, in
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 64), 16);
-    const GridCell *cells = grid_cells(a, lds);
     int lo = 0, hi = J; /* first plane not behind the photon (padding planes, fac' = NaN, count as not) */
     while (lo < hi) {
         const int mid = (lo + hi) >> 1;
@@ -499,7 +513,7 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *lds, in
         if (uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y) continue;
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(g0, p[8 * j + 1], g2, uh, vh, qu, qv);
-        grid_cell_tests(a, cells[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests(a, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
 }
 
@@ -533,7 +547,6 @@ __device__ __forceinline__ void grid_xy_merged(const BakeArgs &a, const char *ld
     const float rx = __builtin_amdgcn_rcpf(d.x), ry = __builtin_amdgcn_rcpf(d.y);
     const float4 *px = (const float4 *)__builtin_assume_aligned(lds + (d.x < 0.0f ? 0 : 64), 16);
     const float4 *py = (const float4 *)__builtin_assume_aligned(lds + 128 * Jx + (d.y < 0.0f ? 0 : 64), 16);
-    const GridCell *cells = grid_cells(a, lds);
     int jx = grid_first_ahead(px, Jx, s.x, rx), jy = grid_first_ahead(py, Jy, s.y, ry);
     float fx = grid_plane_fac(px, jx, Jx, s.x, rx), fy = grid_plane_fac(py, jy, Jy, s.y, ry);
     for (;;) {
@@ -546,7 +559,7 @@ __device__ __forceinline__ void grid_xy_merged(const BakeArgs &a, const char *ld
         if (!(uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y)) {
             uint32_t qu, qv;
             const uint32_t ci = grid_cell(p[0], p[1], g2, uh, vh, qu, qv);
-            grid_cell_tests(a, cells[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
+            grid_cell_tests(a, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
         }
         if (ux) {
             jx++;
@@ -598,7 +611,6 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
     }
     FMGI_CX(0, 1) FMGI_CX(2, 3) FMGI_CX(0, 2) FMGI_CX(1, 3) FMGI_CX(1, 2)
 #undef FMGI_CX
-    const GridCell *cells = grid_cells(a, img);
     for (int k = 0; k < 4; k++) {
         const float f = fk[k];
         if (!(f < INFINITY) || f > L1 * 1.00048828125f) break; /* 1 + 2^-11 */
@@ -612,7 +624,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(g0, g1, g2, uh, vh, qu, qv);
-        grid_cell_tests(a, cells[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests(a, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
 }
 
@@ -635,7 +647,7 @@ __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *i
     const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
     uint32_t qu, qv;
     const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-    grid_cell_tests(a, (grid_cells(a, img))[ci], f, uh, vh, qu, qv, L1, L2, code1, ntest);
+    grid_cell_tests(a, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
 }
 
 __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
@@ -660,7 +672,7 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
         const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-        grid_cell_tests(a, (grid_cells(a, img))[ci], fm, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests(a, load_cell(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
     const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
     if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0>(a, img, s, d, fx, L1, L2, code1, ntest);
@@ -678,7 +690,6 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
     const float su = comp<U>(s), sv = comp<V>(s), du = comp<U>(d), dv = comp<V>(d);
     const float rd = __builtin_amdgcn_rcpf(da);
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 64), 16);
-    const GridCell *cells = grid_cells(a, lds);
     const float4 *recs = (const float4 *)a.grecs;
     for (int j = 0; j < J; j++) {
         const float4 g0 = p[8 * j], g1 = p[8 * j + 1], g2 = p[8 * j + 2];
@@ -686,7 +697,7 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
         if (!(f >= 0.0f)) continue;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         uint32_t qu, qv;
-        const GridCell c = cells[grid_cell(g0, g1, g2, uh, vh, qu, qv)];
+        const GridCell c = load_cell(a, lds, grid_cell(g0, g1, g2, uh, vh, qu, qv));
         if (c.count > 0 && grid_qpass(qu, qv, c.qu0, c.qv0)) fn(c.idx0);
         if (c.count > 1 && grid_qpass(qu, qv, c.qu1, c.qv1)) fn(c.idx1);
         for (int k = 2; k < c.count; k++) {
