@@ -863,11 +863,12 @@ enum { kStreamSliced = 0, kStreamSegments = 1, kStreamBuckets = 2 };
 /* the bucketed stream's pool, in blocks: every code of the chunk, plus one partly filled bucket per wave
    and tile */
 /* pool blocks for `cap` codes: the codes, the sentinel pads (<= 3 per tile and ring flush: a flush per
-   FMGI_RING_CODES codes plus each wave's last), and one partly filled block per wave and tile */
+   FMGI_RING_CODES codes plus each wave's last), one partly filled block per wave and tile, and the
+   blocks a wave holds reserved (< FMGI_BUCKET_ALLOC) */
 static uint64_t bucket_pool_blocks(uint64_t cap, int P, int grid, int block) {
     const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
     const uint64_t pads = (cap / FMGI_RING_CODES + waves) * 3u * (uint64_t)P;
-    return (cap + pads + FMGI_BUCKET_BLOCK - 1) / FMGI_BUCKET_BLOCK + waves * (uint64_t)P + 8;
+    return (cap + pads + FMGI_BUCKET_BLOCK - 1) / FMGI_BUCKET_BLOCK + waves * (uint64_t)(P + FMGI_BUCKET_ALLOC) + 8;
 }
 static uint64_t stream_alloc_codes(uint64_t cap, int P, int grid, int block, int mode) {
     return mode == kStreamBuckets ? bucket_pool_blocks(cap, P, grid, block) * FMGI_BUCKET_BLOCK : cap;

@@ -154,6 +154,9 @@ static_assert(FMGI_STREAM_SLICE_BIG % FMGI_STREAM_SLICE == 0, "run tables are si
 #define FMGI_PRESORT_MAX_TILES 63 /* presorted stream: a tile histogram of one entry per lane        */
 #define FMGI_BUCKET_BLOCK 1024 /* codes per block of the bucketed stream (4 KB; >= a ring, so a ring's run of
                                   one tile spans at most two blocks)                              */
+#ifndef FMGI_BUCKET_ALLOC         /* pool blocks a wave reserves at a time (experiment builds)   */
+#define FMGI_BUCKET_ALLOC 8
+#endif
 #define FMGI_TILE_BITS 11      /* 2048-texel tiles summed in LDS (64 KB: two sum workgroups per
                                   CU; measured 25 ms per 1e9 photons vs 28 ms with 4096, 31 ms with 1024) */
 #define FMGI_MAX_TILES 2048    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */

@@ -1126,16 +1126,54 @@ struct AccStreamT {
     /* at the start of the bake: no wave has an open bucket */
     static __device__ __forceinline__ void bucket_init(const BakeArgs &a, uint32_t *ring) {
         uint4 *info = bucket_info(ring);
-        for (int t = (int)__lane_id(); t < 64; t += 64) info[t] = make_uint4(kNoBlock, BP, 0u, kNoBlock);
+        for (int t = (int)__lane_id(); t < 64; t += 64)
+            info[t] = t == kFree ? make_uint4(0u, 0u, 0u, 0u) : make_uint4(kNoBlock, BP, 0u, kNoBlock);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     }
-    /* a fresh pool block for tile t (kNoBlock if the pool is exhausted: never, by sizing) */
-    static __device__ __forceinline__ uint32_t bucket_alloc(const BakeArgs &a, uint32_t t) {
-        const unsigned long long b = atomicAdd(a.pool_cursor, 1ull);
-        if (b >= a.pool_blocks) return kNoBlock;
-        a.block_tile[b] = t;
-        return (uint32_t)b;
+    /* info[kFree] (no tile: P <= 63): the wave's reserved pool blocks {first, count}. Blocks are reserved
+       kAllocBatch at a time, so a flush that fills a bucket rarely waits for the pool cursor's returning
+       atomic (one per filled bucket before). Every reserved block gets its tile recorded when handed out;
+       the ones still reserved when the bake ends are recorded empty (tile 0, length 0), so the fold's
+       block lists see every block below the cursor. */
+    static constexpr int kFree = 63;
+    static constexpr uint32_t kAllocBatch = FMGI_BUCKET_ALLOC;
+    static __device__ __forceinline__ void bucket_release(const BakeArgs &a, uint4 fl) {
+        for (uint32_t k = (uint32_t)__lane_id(); k < fl.y; k += 64) {
+            a.block_tile[fl.x + k] = 0u;
+            a.block_len[fl.x + k] = 0u;
+        }
+    }
+    /* a fresh pool block for tile t on every live lane with `need` (kNoBlock if the pool is exhausted:
+       never, by sizing). Called where every live lane of the wave is active. */
+    static __device__ __forceinline__ uint32_t bucket_alloc(const BakeArgs &a, uint4 *info, bool need, uint32_t t) {
+        const uint64_t m = __ballot(need);
+        if (m == 0) return kNoBlock;
+        const uint32_t n = (uint32_t)__popcll(m);
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint4 fl = info[kFree];
+        uint32_t b = need && rk < fl.y ? fl.x + rk : kNoBlock;
+        uint4 nf = make_uint4(fl.x + n, fl.y - n, 0u, 0u);
+        if (fl.y < n) { /* (uniform) the rest of the batch, then a new batch */
+            const uint32_t more = n - fl.y, want = more > kAllocBatch ? more : kAllocBatch;
+            const uint64_t live = __ballot(true);
+            const int leader = __ffsll((long long)live) - 1;
+            unsigned long long nb = 0;
+            if ((int)__lane_id() == leader) nb = atomicAdd(a.pool_cursor, (unsigned long long)want);
+            nb = __shfl(nb, leader, 64);
+            const uint64_t have64 = nb < a.pool_blocks ? a.pool_blocks - nb : 0ull;
+            const uint32_t have = (uint32_t)(have64 < want ? have64 : want);
+            if (need && rk >= fl.y && rk - fl.y < have) b = (uint32_t)nb + (rk - fl.y);
+            const uint32_t used = more < have ? more : have;
+            nf = make_uint4(have ? (uint32_t)nb + used : 0u, have - used, 0u, 0u);
+        }
+        if (b != kNoBlock) a.block_tile[b] = t;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if ((int)__lane_id() == __ffsll((long long)__ballot(true)) - 1) info[kFree] = nf;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        return b;
     }
     /* the fallback of an exhausted pool: the code's colour, added to the int64 lightmap with device
        atomics (exact, order-free, as AccFx3) */
@@ -1152,19 +1190,16 @@ struct AccStreamT {
     /* place tile t's padded run of pc codes (pc % 4 == 0; ring run start `start`) in the wave's bucket:
        info[t] becomes {first block, offset in it, run start, second block} (the second only when the
        bucket fills up) */
-    static __device__ __forceinline__ void bucket_place(const BakeArgs &a, uint4 *info, int t, uint32_t start,
-                                                        uint32_t pc) {
-        const uint4 st = info[t];
+    /* (on the live lanes with `act`; called where every live lane of the wave is active) */
+    static __device__ __forceinline__ void bucket_place(const BakeArgs &a, uint4 *info, int t, bool act,
+                                                        uint32_t start, uint32_t pc) {
+        const uint4 st = act ? info[t] : make_uint4(kNoBlock, BP, 0u, kNoBlock);
         const uint32_t room = BP - st.y; /* 0 without an open bucket (y = BP); a multiple of 4 */
-        uint32_t second = kNoBlock;
-        if (pc <= room) {
-            if (pc == room && st.x != kNoBlock) a.block_len[st.x] = BP;
-        } else {
-            if (room && st.x != kNoBlock) a.block_len[st.x] = BP;
-            second = bucket_alloc(a, (uint32_t)t);
-            if (pc - room == BP && second != kNoBlock) a.block_len[second] = BP;
-        }
-        info[t] = make_uint4(st.x, st.y, start, second);
+        const bool spill = act && pc > room;
+        if (act && st.x != kNoBlock && (pc == room || (spill && room))) a.block_len[st.x] = BP;
+        const uint32_t second = bucket_alloc(a, info, spill, (uint32_t)t);
+        if (spill && pc - room == BP && second != kNoBlock) a.block_len[second] = BP;
+        if (act) info[t] = make_uint4(st.x, st.y, start, spill ? second : kNoBlock);
     }
     /* the code of rank rk (a quad: rk % 4 == 0) in tile t's run goes to ... (info as bucket_place left it) */
     static __device__ __forceinline__ uint32_t *bucket_slot(const BakeArgs &a, uint4 inf, uint32_t rk) {
@@ -1257,7 +1292,7 @@ struct AccStreamT {
                     if (cr[h + e] != kSent) ring[o[e]] = cr[h + e];
             }
             for (uint32_t k = cnt; k < pc; k++) ring[start + k] = kSent;
-            if (cnt) bucket_place(a, info, (int)r, start, pc);
+            bucket_place(a, info, (int)r, cnt != 0, start, pc);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
             for (uint32_t q = r; q < quads; q += 64) {
@@ -1273,10 +1308,12 @@ struct AccStreamT {
             for (uint32_t k = r; k < n; k += nl) atomicAdd(&hist[ring[k] >> shift], 1u);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            for (int t = (int)r; t < P; t += (int)nl) {
-                const uint32_t cnt = hist[t], pc = (cnt + 3u) & ~3u;
-                if (cnt) bucket_place(a, info, t, 0u, pc);
-                for (uint32_t k = cnt; k < pc; k++) bucket_store(a, info[t], k, kSent);
+            for (int t0 = 0; t0 < P; t0 += (int)nl) { /* (uniform trip count: bucket_place is wave-wide) */
+                const int t = t0 + (int)r;
+                const uint32_t cnt = t < P ? hist[t] : 0u, pc = (cnt + 3u) & ~3u;
+                bucket_place(a, info, t, cnt != 0, 0u, pc);
+                if (t < P)
+                    for (uint32_t k = cnt; k < pc; k++) bucket_store(a, info[t], k, kSent);
             }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
@@ -1305,6 +1342,7 @@ struct AccStreamT {
             const uint4 inf = info[t];
             if (inf.x != kNoBlock && inf.y < BP) a.block_len[inf.x] = inf.y;
         }
+        bucket_release(a, info[kFree]);
     }
 
     static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, uint32_t *ring, bool dep,
