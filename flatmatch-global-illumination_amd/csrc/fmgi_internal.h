@@ -151,6 +151,11 @@ static_assert(FMGI_STREAM_SLICE_BIG % FMGI_STREAM_SLICE == 0, "run tables are si
 #define FMGI_RING_HIST (FMGI_RING_CODES + FMGI_RING_PAD)      /* tile histogram (64)                     */
 #define FMGI_RING_INFO (FMGI_RING_HIST + 64)                  /* bucketed stream's per-tile info (64 x 16 B) */
 #define FMGI_RING_STRIDE (FMGI_RING_INFO + 256)               /* per-wave LDS dwords                     */
+#ifndef FMGI_SUBHIST  /* bucketed stream (experiment builds): the flush counts and ranks codes in k tile */
+#define FMGI_SUBHIST 1 /* histograms, one per lane mod k, after the info table. k = 2 or 4: box200 bake */
+#endif                 /* 77.33 / 77.46 ms against 77.32 with the one (profiles/r04/s21)              */
+#define FMGI_RING_SUB FMGI_RING_STRIDE                         /* FMGI_SUBHIST x 64 counters            */
+#define FMGI_RING_STRIDE_BUCKET (FMGI_RING_STRIDE + (FMGI_SUBHIST > 1 ? FMGI_SUBHIST * 64 : 0))
 #define FMGI_PRESORT_MAX_TILES 63 /* presorted stream: a tile histogram of one entry per lane        */
 #define FMGI_BUCKET_BLOCK 1024 /* codes per block of the bucketed stream (4 KB; >= a ring, so a ring's run of
                                   one tile spans at most two blocks)                              */

@@ -1265,12 +1265,29 @@ struct AccStreamT {
                 for (int e = 0; e < CPL; e++) cr[e] = CPL * r + e < n ? ring[CPL * r + e] : kSent;
             }
             const uint32_t ov = ring[FMGI_RING_CODES + r]; /* the overflow (append moves it after the flush) */
+            /* counts and ranks in FMGI_SUBHIST histograms, lane mod FMGI_SUBHIST each: the adds of one
+               instruction meet on fewer equal addresses (46 tiles under 64 lanes, a same-address LDS
+               atomic serialises) */
+            constexpr int NS = FMGI_SUBHIST > 1 ? FMGI_SUBHIST : 1;
+            uint32_t *sub = NS > 1 ? ring + FMGI_RING_SUB : hist;
+            uint32_t *mine = sub + (NS > 1 ? 64 * (r % NS) : 0);
+            if (NS > 1) {
+#pragma unroll
+                for (int g = 0; g < NS; g++) sub[64 * g + r] = 0u;
+                __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+            }
 #pragma unroll
             for (int e = 0; e < CPL; e++)
-                if (cr[e] != kSent) atomicAdd(&hist[cr[e] >> shift], 1u);
+                if (cr[e] != kSent) atomicAdd(&mine[cr[e] >> shift], 1u);
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
-            const uint32_t cnt = (int)r < P ? hist[r] : 0u; /* lane t: tile t */
+            uint32_t cg[NS], cnt = 0; /* lane t: tile t's count in each histogram */
+#pragma unroll
+            for (int g = 0; g < NS; g++) {
+                cg[g] = (int)r < P ? sub[64 * g + r] : 0u;
+                cnt += cg[g];
+            }
             const uint32_t pc = (cnt + 3u) & ~3u;
             uint32_t incl = pc;
             for (int off = 1; off < 64; off <<= 1) {
@@ -1278,7 +1295,14 @@ struct AccStreamT {
                 if ((int)r >= off) incl += o;
             }
             const uint32_t start = incl - pc, quads = __shfl(incl, 63, 64) >> 2;
-            if ((int)r < P) hist[r] = start;
+            if ((int)r < P) {
+                uint32_t run = start;
+#pragma unroll
+                for (int g = 0; g < NS; g++) {
+                    sub[64 * g + r] = run;
+                    run += cg[g];
+                }
+            }
             __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
             __builtin_amdgcn_wave_barrier();
 #pragma unroll
@@ -1286,7 +1310,7 @@ struct AccStreamT {
                 uint32_t o[SC];
 #pragma unroll
                 for (int e = 0; e < SC; e++)
-                    o[e] = cr[h + e] != kSent ? atomicAdd(&hist[cr[h + e] >> shift], 1u) : 0u;
+                    o[e] = cr[h + e] != kSent ? atomicAdd(&mine[cr[h + e] >> shift], 1u) : 0u;
 #pragma unroll
                 for (int e = 0; e < SC; e++)
                     if (cr[h + e] != kSent) ring[o[e]] = cr[h + e];
@@ -1580,6 +1604,10 @@ struct HasAppend<AccLines> {
 template <class Acc>
 __device__ __forceinline__ uint32_t *acc_region(char *lds, const BakeArgs &a) {
     return (uint32_t *)(lds + a.ring_off) + (threadIdx.x >> 6) * FMGI_RING_STRIDE;
+}
+template <>
+__device__ __forceinline__ uint32_t *acc_region<AccBucket>(char *lds, const BakeArgs &a) {
+    return (uint32_t *)(lds + a.ring_off) + (threadIdx.x >> 6) * FMGI_RING_STRIDE_BUCKET;
 }
 template <>
 __device__ __forceinline__ uint32_t *acc_region<AccLines>(char *lds, const BakeArgs &a) {
@@ -2070,7 +2098,8 @@ size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
     if (accum == kAccLines) return img + (size_t)FMGI_LINES_DWORDS * 4;
-    return img + ((accum == 4 || accum == kAccBucket) ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
+    if (accum == kAccBucket) return img + (size_t)(block / 64) * FMGI_RING_STRIDE_BUCKET * 4;
+    return img + (accum == 4 ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
 
 /* a bake launch of more than 64 KiB of dynamic LDS (scan image + staged tables + rings, fmgi_api.cpp
