@@ -287,12 +287,14 @@ static uint32_t grid_bounds(float c, float hw, float o, float inv, int cell) {
     return grid_q(a, o, inv, cell) | (grid_q(b, o, inv, cell) << 16);
 }
 
-GridBuild build_grid(const FilterBuild &fb) {
+/* cells per record the grid's cost model may spend (FMGI_GRID_CPR, experiments; 0 if unset) */
+static int grid_cpr_env() {
+    const char *ce = getenv("FMGI_GRID_CPR");
+    return ce && atoi(ce) >= 1 && atoi(ce) <= 64 ? atoi(ce) : 0;
+}
+
+GridBuild build_grid(const FilterBuild &fb, int cells_per_record) {
     GridBuild gb;
-    /* cells per record the cost model may spend (FMGI_GRID_CPR, experiments: coarser grids are smaller) */
-    int cells_per_record = 16;
-    if (const char *ce = getenv("FMGI_GRID_CPR"))
-        if (atoi(ce) >= 1 && atoi(ce) <= 64) cells_per_record = atoi(ce);
     gb.cells.push_back(GridCell{kGridNoRec, kGridNoRec, kGridNoRec, kGridNoRec, 0, -1, -1, 0}); /* cell 0: empty */
     std::vector<GridPlane> planes[3][2];
     for (int a = 0; a < 3; a++) {
@@ -642,6 +644,7 @@ struct fmgi_context {
     int gimg_bytes = 0;
     int gJ[3] = {0, 0, 0};
     GridCell *d_gcells = nullptr;
+    bool cells_lds = false;       /* the grid was built coarse to be staged in LDS (closed boxes) */
     char *d_himg = nullptr;       /* ScanHybrid (default instance): the grid's plane image, then the wall pairs */
     int himg_bytes = 0;
     char *d_himg_full = nullptr;  /* ... the floor-plan walk and FMGI_FILTER_PK=0 builds: filter image | plane
@@ -1048,7 +1051,27 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->h_fimg = fb.img;
     c->ngeneral = (int)fb.general.size();
     c->margin = fb.margin;
-    GridBuild gb = build_grid(fb);
+    GridBuild gb = build_grid(fb, grid_cpr_env() ? grid_cpr_env() : 16);
+    /* closed boxes (one plane per class on each axis, the closed-box instance): the coarsest grid of 5 or 4
+       cells per record whose cells fit in 32 KB, staged in LDS beside the rings (plan_stage) when that
+       keeps the wave count: every cell lookup an LDS read. box200: 951 cells of 32 B, bake 77.4 -> 74.9 ms
+       (~2 record tests per scan instead of ~1.5, profiles/r04/s23). FMGI_CELLS_LDS=0 keeps the
+       16-per-record grid in global memory. */
+    c->cells_lds = false;
+    {
+        const char *cl = getenv("FMGI_CELLS_LDS");
+        if (!grid_cpr_env() && !(cl && atoi(cl) == 0) && gb.J[0] == 1 && gb.J[1] == 1 && gb.J[2] == 1 &&
+            !getenv("FMGI_NO_AXES")) {
+            for (int cpr : {5, 4}) {
+                GridBuild g = build_grid(fb, cpr);
+                if (g.cells.size() * sizeof(GridCell) <= 32768) {
+                    gb = g;
+                    c->cells_lds = true;
+                    break;
+                }
+            }
+        }
+    }
     for (int a = 0; a < 3; a++) c->gJ[a] = gb.J[a];
     c->gimg_bytes = (int)(gb.img.size() * sizeof(GridPlane));
     c->grid_cells = (int)gb.cells.size();
@@ -1326,9 +1349,12 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     /* (768-lane workgroups measured pathological for every instance built for 4 waves/SIMD: box200 bake
        1.6-2.2 s instead of 0.05-0.08 s, profiles/r04/s7; not offered) */
     const int blocks_all[] = {256, 512, 1024};
-    /* the grid cells (experiments, FMGI_CELLS_LDS=1: every cell lookup an LDS read instead of an L2 one) */
+    /* the grid cells in LDS: every cell lookup an LDS read instead of an L2 one. The closed boxes' coarse
+       grid asks for it (kept only if the wave count holds); FMGI_CELLS_LDS=1 forces it for any grid or
+       hybrid scan that fits, 0 turns it off (experiments) */
     const char *ce = getenv("FMGI_CELLS_LDS");
-    bool cells = ce && atoi(ce) == 1 && (kernel == FMGI_KERNEL_GRID || kernel == FMGI_KERNEL_HYBRID);
+    const bool cells_forced = ce && atoi(ce) == 1 && (kernel == FMGI_KERNEL_GRID || kernel == FMGI_KERNEL_HYBRID);
+    bool cells = cells_forced || (!ce && c->cells_lds && kernel == FMGI_KERNEL_GRID);
     auto best = [&](bool rects, int &bb, int &bw) {
         const int bytes = stage_bytes(c, kernel, rects, srcs, cells, nullptr, nullptr);
         bb = p.block;
@@ -1349,10 +1375,18 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
            walls staged 77.6 ms, 20 waves without 123.8 ms), not two */
         rects = rects_mode == 1 ? w1 > 0 : (w1 > 0 && w1 >= std::min(w0, 16));
     }
-    if (cells && (rects ? w1 : w0) <= 0) { /* the cells do not fit beside the rest: not staged */
+    if (cells) { /* staged only if they fit (forced) or keep the wave count of the plan without them */
+        const int wc = rects ? w1 : w0;
         cells = false;
-        best(false, b0, w0);
-        if (rects) best(true, b1, w1);
+        int nb0, nw0, nb1 = 0, nw1 = 0;
+        best(false, nb0, nw0);
+        if (rects) best(true, nb1, nw1);
+        const int wn = rects ? nw1 : nw0;
+        if (wc > 0 && (cells_forced || wc >= wn)) {
+            cells = true;
+        } else {
+            b0 = nb0, w0 = nw0, b1 = nb1, w1 = nw1;
+        }
     }
     p.block = rects ? b1 : b0;
     p.bytes = stage_bytes(c, kernel, rects, srcs, cells, &p.rects_off, &p.srcs_off, &p.cells_off);

@@ -252,7 +252,9 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     st = ctx.stats()
     assert st["photons"] == 100 * n
     assert st["deposits"] + st["escapes"] == st["scans"]
-    assert st["tests"] < 2 * st["scans"]  # the grid's phase 1: ~1.5 record tests per scan in a closed box
+    # the grid's phase 1 in a closed box: ~2 record tests per scan on the coarse grid staged in LDS (5 cells
+    # per record), ~1.5 on the 16-per-record grid (FMGI_CELLS_LDS=0)
+    assert st["tests"] < 2.5 * st["scans"]
     # energy accounting: the lightmap total equals the sum over deposits (every deposit >= 0.25)
     assert int(a[:, :3].astype(np.float64).sum()) >= st["deposits"] * 3 * (2**25 // 4)
     ctx.close()
