@@ -1298,12 +1298,12 @@ FMGI_API int64_t fmgi_get_plan(fmgi_context *c, fmgi_launch *out, int64_t cap) {
  */
 struct StagePlan {
     int block = 256;
-    int bytes = 0;                   /* staged blob = image (16-B aligned) | rects | srcs | cells */
-    int rects_off = -1, srcs_off = -1, cells_off = -1;
+    int bytes = 0;                   /* staged blob = image (16-B aligned) | rects | srcs | cells | overflow */
+    int rects_off = -1, srcs_off = -1, cells_off = -1, grecs_off = -1, gidx_off = -1;
 };
 
 static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, bool cells, int *roff, int *soff,
-                       int *coff = nullptr) {
+                       int *coff = nullptr, int *groff = nullptr, int *gioff = nullptr) {
     int off = (image_bytes(c, kernel) + 15) & ~15;
     if (roff) *roff = rects ? off : -1;
     if (rects) off += c->nrects * (int)sizeof(RectLds);
@@ -1312,7 +1312,16 @@ static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs,
     off = (off + 15) & ~15;
     if (coff) *coff = cells ? off : -1;
     if (cells) off += c->grid_cells * (int)sizeof(GridCell);
-    return off;
+    /* with the cells (FMGI_GRECS_LDS=1, experiments), the overflow records of cells of more than two
+       (float4) and their rect indices: box200 bake 76.65 -> 77.16 ms (profiles/r04/s26), so by default
+       they stay in global memory */
+    const char *ge = getenv("FMGI_GRECS_LDS");
+    const bool ov = cells && ge && atoi(ge) == 1;
+    if (groff) *groff = ov ? off : -1;
+    if (ov) off += c->grid_entries * 16;
+    if (gioff) *gioff = ov ? off : -1;
+    if (ov) off += c->grid_entries * 4;
+    return (off + 15) & ~15;
 }
 
 /* the kernel instance a bake of `kernel` launches: the grid scan of a closed box (one plane per axis and
@@ -1389,7 +1398,8 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
         }
     }
     p.block = rects ? b1 : b0;
-    p.bytes = stage_bytes(c, kernel, rects, srcs, cells, &p.rects_off, &p.srcs_off, &p.cells_off);
+    p.bytes = stage_bytes(c, kernel, rects, srcs, cells, &p.rects_off, &p.srcs_off, &p.cells_off, &p.grecs_off,
+                          &p.gidx_off);
     return p;
 }
 
@@ -1549,9 +1559,10 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.fimg_bytes = c->fimg_bytes;
         for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
     }
-    a.rects_off = a.srcs_off = a.cells_off = -1;
+    a.rects_off = a.srcs_off = a.cells_off = a.grecs_off = a.gidx_off = -1;
     if (sp.rects_off >= 0 || sp.srcs_off >= 0 || sp.cells_off >= 0) { /* the blob: image | rects | srcs | cells */
-        const uint64_t key = (c->scene_gen << 8) | (kernel == FMGI_KERNEL_HYBRID && hybrid_full(c) ? 0x40u : 0u) |
+        const uint64_t key = (c->scene_gen << 9) | (sp.grecs_off >= 0 ? 0x100u : 0u) |
+                             (kernel == FMGI_KERNEL_HYBRID && hybrid_full(c) ? 0x40u : 0u) |
                              ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) | (sp.srcs_off >= 0 ? 1u : 0u) |
                              (sp.cells_off >= 0 ? 0x80u : 0u);
         if (c->blob_key != key) {
@@ -1587,9 +1598,16 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             if (sp.srcs_off >= 0)
                 HIPCHK(hipMemcpyAsync(c->d_blob + sp.srcs_off, c->d_srcs, (size_t)c->nsrcs * sizeof(SrcDev),
                                       hipMemcpyDeviceToDevice, s));
-            if (sp.cells_off >= 0)
+            if (sp.cells_off >= 0) {
                 HIPCHK(hipMemcpyAsync(c->d_blob + sp.cells_off, c->d_gcells, (size_t)c->grid_cells * sizeof(GridCell),
                                       hipMemcpyDeviceToDevice, s));
+                if (sp.grecs_off >= 0) {
+                    HIPCHK(hipMemcpyAsync(c->d_blob + sp.grecs_off, c->d_grecs, (size_t)c->grid_entries * 16,
+                                          hipMemcpyDeviceToDevice, s));
+                    HIPCHK(hipMemcpyAsync(c->d_blob + sp.gidx_off, c->d_gidx, (size_t)c->grid_entries * 4,
+                                          hipMemcpyDeviceToDevice, s));
+                }
+            }
             c->blob_key = key;
         }
         a.fimg = c->d_blob;
@@ -1597,6 +1615,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.rects_off = sp.rects_off;
         a.srcs_off = sp.srcs_off;
         a.cells_off = sp.cells_off;
+        a.grecs_off = sp.grecs_off;
+        a.gidx_off = sp.gidx_off;
     }
     a.general = c->d_general;
     a.ngeneral = c->ngeneral;

@@ -94,6 +94,8 @@ struct BakeArgs {
        the scans' winners) and of the SrcDev table (every photon's emission); -1: read from global memory */
     int rects_off, srcs_off;
     int cells_off;        /* >= 0: byte offset of a copy of the grid cells (GridCell) in the staged blob */
+    int grecs_off;        /* >= 0 (with cells_off): byte offsets of copies of the grid's overflow records */
+    int gidx_off;         /*   (float4) and their rect indices (int32) in the staged blob             */
     int gJ[3];            /* ScanHybrid: the grid's plane pairs per axis; its plane image is at LDS  */
     int hyb_off;          /* offset hyb_off after the filter image (fimg = filter image || plane image) */
     int plan_off;         /* ScanHybridPlan: byte offset of the floor plan in the image (-1: none)      */

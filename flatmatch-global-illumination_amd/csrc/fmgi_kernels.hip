@@ -463,16 +463,28 @@ __device__ __forceinline__ void grid_recq(float f, uint32_t qu, uint32_t qv, uin
 
 /* the candidate tests of one cell: its two inline records (quantized bounds; absent ones are never
    candidates), then its overflow records (float, rare); code1 receives the winner's rect index */
-__device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const GridCell &c, float f, float uh, float vh,
-                                                uint32_t qu, uint32_t qv, float &L1, float &L2, int &code1,
-                                                unsigned &ntest) {
+__device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const char *lds, const GridCell &c, float f,
+                                                float uh, float vh, uint32_t qu, uint32_t qv, float &L1, float &L2,
+                                                int &code1, unsigned &ntest) {
     ntest += (unsigned)c.count;
     grid_recq(f, qu, qv, c.qu0, c.qv0, c.idx0 | a.grid_code_or, L1, L2, code1);
     grid_recq(f, qu, qv, c.qu1, c.qv1, c.idx1 | a.grid_code_or, L1, L2, code1);
     if (c.count > 2) {
-        const float4 *recs = (const float4 *)a.grecs;
-        for (int k = 2; k < c.count; k++)
-            grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2] | a.grid_code_or, L1, L2, code1);
+        if (uni(a.grecs_off) >= 0) { /* the overflow records staged beside the cells */
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const __attribute__((address_space(3))) char *l = (const __attribute__((address_space(3))) char *)lds;
+            const __attribute__((address_space(3))) f4v *recs =
+                (const __attribute__((address_space(3))) f4v *)(l + a.grecs_off);
+            const __attribute__((address_space(3))) int *ix = (const __attribute__((address_space(3))) int *)(l + a.gidx_off);
+            for (int k = 2; k < c.count; k++) {
+                const f4v r = recs[c.rest + k - 2];
+                grid_rec(f, uh, vh, make_float4(r.x, r.y, r.z, r.w), ix[c.rest + k - 2] | a.grid_code_or, L1, L2, code1);
+            }
+        } else {
+            const float4 *recs = (const float4 *)a.grecs;
+            for (int k = 2; k < c.count; k++)
+                grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2] | a.grid_code_or, L1, L2, code1);
+        }
     }
 }
 
@@ -513,7 +525,7 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *lds, in
         if (uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y) continue;
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(g0, p[8 * j + 1], g2, uh, vh, qu, qv);
-        grid_cell_tests(a, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests(a, lds, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
 }
 
@@ -559,7 +571,7 @@ __device__ __forceinline__ void grid_xy_merged(const BakeArgs &a, const char *ld
         if (!(uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y)) {
             uint32_t qu, qv;
             const uint32_t ci = grid_cell(p[0], p[1], g2, uh, vh, qu, qv);
-            grid_cell_tests(a, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+            grid_cell_tests(a, lds, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
         }
         if (ux) {
             jx++;
@@ -624,7 +636,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(g0, g1, g2, uh, vh, qu, qv);
-        grid_cell_tests(a, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests(a, img, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
 }
 
@@ -647,7 +659,7 @@ __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *i
     const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
     uint32_t qu, qv;
     const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-    grid_cell_tests(a, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+    grid_cell_tests(a, img, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
 }
 
 __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
@@ -672,7 +684,7 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
         const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-        grid_cell_tests(a, load_cell(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests(a, img, load_cell(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
     const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
     if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0>(a, img, s, d, fx, L1, L2, code1, ntest);

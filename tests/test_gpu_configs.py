@@ -102,7 +102,7 @@ def _host_threads():
 
 
 @pytest.mark.timeout(900)
-def test_config3_full_lightmap_exact(torch_cuda, box200, offsets):
+def test_config3_full_lightmap_exact(torch_cuda, box200, offsets, capsys):
     """BASELINE config 3 -- the headline bench's step -- at full size: all 10,000,128 work items
     (1,000,012,800 photons, 391 launches) through the default path (closed-box grid scan, bucketed stream,
     one chunk), the whole int64 lightmap and the photon / scan / deposit / escape counters equal to the
@@ -119,7 +119,17 @@ def test_config3_full_lightmap_exact(torch_cuda, box200, offsets):
     st = ctx.stats()
     ctx.close()
     assert st["stream_overflow"] == 0
-    olm, ost = O.bake_port(box200, L, 0, n, nthreads=_host_threads())
+    # the oracle in 16 item ranges (its lightmap is an exact int64 sum, so the parts add up to the whole),
+    # a progress line after each: ~190 s of host work must not look like a silent, hung run
+    olm, ost = None, {}
+    cuts = [n * k // 16 for k in range(17)]
+    for k in range(16):
+        plm, pst = O.bake_port(box200, L, cuts[k], cuts[k + 1], nthreads=_host_threads())
+        olm = plm if olm is None else olm + plm
+        for key in ("photons", "scans", "deposits", "escapes"):
+            ost[key] = ost.get(key, 0) + pst[key]
+        with capsys.disabled():
+            print(f"\n  config 3 oracle: items {cuts[k + 1]:,} of {n:,}", flush=True)
     assert np.array_equal(lm[:, :3], olm)
     assert not lm[:, 3].any()
     for k in ("photons", "scans", "deposits", "escapes"):
