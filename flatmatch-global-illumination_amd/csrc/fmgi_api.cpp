@@ -253,6 +253,7 @@ struct GridBuild {
     std::vector<GridPlane> img; /* per axis a: J[a] pairs {+a plane j, -a plane j} */
     int J[3] = {0, 0, 0};
     std::vector<GridCell> cells;
+    std::vector<GridCellF> cellsF; /* the same cells with float inline records (general grid walks) */
     std::vector<float> recs; /* overflow records {cu, hwu, cv, hwv} (cell entries 2..count) */
     std::vector<int32_t> idx;
 };
@@ -296,6 +297,7 @@ static int grid_cpr_env() {
 GridBuild build_grid(const FilterBuild &fb, int cells_per_record) {
     GridBuild gb;
     gb.cells.push_back(GridCell{kGridNoRec, kGridNoRec, kGridNoRec, kGridNoRec, 0, -1, -1, 0}); /* cell 0: empty */
+    gb.cellsF.push_back(GridCellF{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0, -1, -1, 0});
     std::vector<GridPlane> planes[3][2];
     for (int a = 0; a < 3; a++) {
         for (int c = 0; c < 2; c++) {
@@ -415,11 +417,21 @@ GridBuild build_grid(const FilterBuild &fb, int cells_per_record) {
                         gc.qv1 = grid_bounds(b[1]->cv, b[1]->hwv, g.v0, g.iv, iv);
                         gc.idx1 = b[1]->idx;
                     }
+                    GridCellF gf{0.f, -1.f, 0.f, -1.f, 0.f, -1.f, 0.f, -1.f, (int32_t)b.size(), -1, -1, gc.rest};
+                    if (b.size() > 0) {
+                        gf.cu0 = b[0]->cu, gf.hwu0 = b[0]->hwu, gf.cv0 = b[0]->cv, gf.hwv0 = b[0]->hwv;
+                        gf.idx0 = b[0]->idx;
+                    }
+                    if (b.size() > 1) {
+                        gf.cu1 = b[1]->cu, gf.hwu1 = b[1]->hwu, gf.cv1 = b[1]->cv, gf.hwv1 = b[1]->hwv;
+                        gf.idx1 = b[1]->idx;
+                    }
                     for (size_t k = 2; k < b.size(); k++) {
                         gb.recs.insert(gb.recs.end(), {b[k]->cu, b[k]->hwu, b[k]->cv, b[k]->hwv});
                         gb.idx.push_back(b[k]->idx);
                     }
                     gb.cells.push_back(gc);
+                    gb.cellsF.push_back(gf);
                 }
                 planes[a][c].push_back(g);
             }
@@ -644,6 +656,7 @@ struct fmgi_context {
     int gimg_bytes = 0;
     int gJ[3] = {0, 0, 0};
     GridCell *d_gcells = nullptr;
+    GridCellF *d_gcellsF = nullptr;
     bool cells_lds = false;       /* the grid was built coarse to be staged in LDS (closed boxes) */
     char *d_himg = nullptr;       /* ScanHybrid (default instance): the grid's plane image, then the wall pairs */
     int himg_bytes = 0;
@@ -765,6 +778,7 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_general);
     hipFree(c->d_gimg);
     hipFree(c->d_gcells);
+    hipFree(c->d_gcellsF);
     hipFree(c->d_himg);
     hipFree(c->d_himg_full);
     hipFree(c->d_blob);
@@ -1143,14 +1157,17 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     }
     hipFree(c->d_gimg);
     hipFree(c->d_gcells);
+    hipFree(c->d_gcellsF);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
     c->d_gimg = nullptr;
     c->d_gcells = nullptr;
+    c->d_gcellsF = nullptr;
     c->d_grecs = nullptr;
     c->d_gidx = nullptr;
     HIPCHK(upload(&c->d_gimg, gb.img));
     HIPCHK(upload(&c->d_gcells, gb.cells));
+    HIPCHK(upload(&c->d_gcellsF, gb.cellsF));
     {   /* ScanHybrid's full image: the filter image (a multiple of 64 B), the plane image, the plan, the pairs */
         std::vector<char> both((size_t)c->himg_full_bytes);
         memcpy(both.data(), fb.img.data(), (size_t)c->fimg_bytes);
@@ -1533,6 +1550,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.fimg_bytes = c->gimg_bytes;
         for (int k = 0; k < 3; k++) a.fJ[k] = c->gJ[k];
         a.gcells = c->d_gcells;
+        a.gcellsF = c->d_gcellsF;
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
         a.grid_axes = grid_axes_scene(c) ? 1 : 0;
@@ -1547,6 +1565,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             a.gJ[k] = c->gJ[k];
         }
         a.gcells = c->d_gcells;
+        a.gcellsF = c->d_gcellsF;
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
         a.grid_code_or = 0x40000000;

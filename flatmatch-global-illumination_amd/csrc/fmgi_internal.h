@@ -58,6 +58,15 @@ struct GridCell {
 };
 static_assert(sizeof(GridCell) == 32, "GridCell must be 32 B");
 constexpr uint32_t kGridNoRec = 0xFFFFu; /* lo 0xFFFF, hi 0: no q passes */
+/* the same cell with float records (centre, half-extent; absent: half-extent -1), read by the general
+   grid walks (many planes per scan), where the 16-bit cell coordinates cost more per visited plane than
+   the 16 B they save */
+struct GridCellF {
+    float cu0, hwu0, cv0, hwv0;
+    float cu1, hwu1, cv1, hwv1;
+    int32_t count, idx0, idx1, rest;
+};
+static_assert(sizeof(GridCellF) == 48, "GridCellF must be 48 B");
 
 struct BakeArgs {
     const RectDev *rects;
@@ -86,6 +95,7 @@ struct BakeArgs {
        (GridCell), the overflow records (float4 {cu, hwu, cv, hwv}) and their rect indices live in
        global memory */
     const void *gcells;
+    const void *gcellsF;  /* GridCellF, same indices */
     const float *grecs;
     const int32_t *gridx;
     int grid_axes; /* fJ == {1, 1, 1}: slot a of the image is axis a (ScanGrid's grid_phase1_axes) */

@@ -488,6 +488,31 @@ __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const char *l
     }
 }
 
+/* The general walks' cell (many planes per scan): the index alone (no 16-bit cell coordinates), and the
+   cell's float inline records (GridCellF), as before the 32-B cells: 57 ms against 71 ms on the 30-room
+   layout (profiles/r04/s31-s32) */
+__device__ __forceinline__ uint32_t grid_cell_idx(const float4 g0, const float4 g1, const float4 g2, float uh, float vh) {
+    const float tu = __builtin_amdgcn_fmed3f((uh - g0.y) * g0.w, 0.0f, g1.y);
+    const float tv = __builtin_amdgcn_fmed3f((vh - g0.z) * g1.x, 0.0f, g1.z);
+    return (uint32_t)__float_as_int(g2.y) + __umul24((uint32_t)tv, (uint32_t)__float_as_int(g1.w)) + (uint32_t)tu;
+}
+__device__ __forceinline__ void grid_cell_tests_f(const BakeArgs &a, uint32_t ci, float f, float uh, float vh,
+                                                  float &L1, float &L2, int &code1, unsigned &ntest) {
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const gptr<f4v> cp = (gptr<f4v>)a.gcellsF + 3 * ci;
+    const f4v r0 = cp[0], r1 = cp[1], r2 = cp[2];
+    const int count = __float_as_int(r2.x), idx0 = __float_as_int(r2.y), idx1 = __float_as_int(r2.z),
+              rest = __float_as_int(r2.w);
+    ntest += (unsigned)count;
+    grid_rec(f, uh, vh, make_float4(r0.x, r0.y, r0.z, r0.w), idx0 | a.grid_code_or, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(r1.x, r1.y, r1.z, r1.w), idx1 | a.grid_code_or, L1, L2, code1);
+    if (count > 2) {
+        const float4 *recs = (const float4 *)a.grecs;
+        for (int k = 2; k < count; k++)
+            grid_rec(f, uh, vh, recs[rest + k - 2], a.gridx[rest + k - 2] | a.grid_code_or, L1, L2, code1);
+    }
+}
+
 /*
  * Phase 1 of ScanGrid on the planes of axis A: per facing plane, fac' and the hit point once, the cell
  * it falls in, and the records of that cell (the first two loaded together with no wait in between).
@@ -523,9 +548,7 @@ __device__ __forceinline__ void grid_axis(const BakeArgs &a, const char *lds, in
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
         const float4 g2 = p[8 * j + 2], g3 = p[8 * j + 3];
         if (uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y) continue;
-        uint32_t qu, qv;
-        const uint32_t ci = grid_cell(g0, p[8 * j + 1], g2, uh, vh, qu, qv);
-        grid_cell_tests(a, lds, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests_f(a, grid_cell_idx(g0, p[8 * j + 1], g2, uh, vh), f, uh, vh, L1, L2, code1, ntest);
     }
 }
 
@@ -569,9 +592,7 @@ __device__ __forceinline__ void grid_xy_merged(const BakeArgs &a, const char *ld
         const float uh = fmaf(ux ? d.y : d.x, f, ux ? s.y : s.x), vh = fmaf(d.z, f, s.z);
         const float4 g2 = p[2], g3 = p[3];
         if (!(uh < g2.z || uh > g2.w || vh < g3.x || vh > g3.y)) {
-            uint32_t qu, qv;
-            const uint32_t ci = grid_cell(p[0], p[1], g2, uh, vh, qu, qv);
-            grid_cell_tests(a, lds, load_cell(a, lds, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+            grid_cell_tests_f(a, grid_cell_idx(p[0], p[1], g2, uh, vh), f, uh, vh, L1, L2, code1, ntest);
         }
         if (ux) {
             jx++;
@@ -634,9 +655,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
         const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * q + (da < 0.0f ? 0 : 64), 16);
         const float4 g0 = p[0], g1 = p[1], g2 = p[2];
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        uint32_t qu, qv;
-        const uint32_t ci = grid_cell(g0, g1, g2, uh, vh, qu, qv);
-        grid_cell_tests(a, img, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests_f(a, grid_cell_idx(g0, g1, g2, uh, vh), f, uh, vh, L1, L2, code1, ntest);
     }
 }
 
