@@ -22,6 +22,8 @@
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
 
+#include <algorithm>
+
 #include "fmgi_internal.h"
 
 namespace {
@@ -453,12 +455,176 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
     }
 }
 
+/* The binning pass of the dense stream (kAccDense, BakeArgs::presort == 3): the bake wrote one code or
+   sentinel per lane and iteration, in no order; k_bin groups them into the bucket layout k_bucket_fold reads
+   (pool blocks of FMGI_BUCKET_BLOCK codes, each holding one fold tile's codes, its tile and length recorded).
+   Persistent workgroups of 1024 lanes take 8192-code batches in turn. Per batch: each wave counts its 512
+   codes per tile in its own LDS histogram; a scan over (tile, wave) gives every wave's range in the batch
+   sorted by tile; the codes are scattered into that order in LDS (32 KB); one lane per tile appends the
+   tile's run to the workgroup's open block of that tile, taking new blocks (one pool-cursor atomic per tile
+   and batch when the run overflows); then all lanes copy the sorted batch out, consecutive lanes to
+   consecutive codes of one run. Runs average 8192 / P codes (~178 on box200), so the stores are whole
+   lines. HBM traffic per code: 4 B read, 4 B written. A pool too small (never, by sizing) sends the codes
+   through exact int64 atomics into the lightmap, as the bake's bucket fallback. */
+constexpr int kBinThreads = 1024, kBinPer = 8, kBinBatch = kBinThreads * kBinPer;
+constexpr uint32_t kNoBlk = 0xFFFFFFFFu;
+
+__device__ __forceinline__ void bin_atomic(const uint4 *colpack, unsigned long long *lm, uint32_t code) {
+    const uint4 cc = colpack[code & 1023];
+    unsigned long long *q = lm + 4 * (size_t)(code >> 10);
+    const unsigned long long r = cc.x;
+    atomicAdd(q + 0, r);
+    atomicAdd(q + 1, r + (unsigned long long)(long long)(int32_t)cc.y);
+    atomicAdd(q + 2, r + (unsigned long long)(long long)(int32_t)cc.z);
+}
+
+__global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restrict__ dense,
+                                                     const unsigned long long *__restrict__ n_ptr, uint64_t cap,
+                                                     int P, uint32_t *__restrict__ pool,
+                                                     uint32_t *__restrict__ block_tile, uint32_t *__restrict__ block_len,
+                                                     unsigned long long *__restrict__ pool_cursor, uint64_t pool_blocks,
+                                                     const uint4 *__restrict__ colpack, unsigned long long *__restrict__ lm) {
+    constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
+    extern __shared__ __attribute__((aligned(16))) uint32_t stage[]; /* kBinBatch codes */
+    __shared__ uint32_t hist[16][64];
+    __shared__ uint32_t ttot[64], tstart[64];
+    __shared__ uint2 info[64];  /* per tile: the workgroup's open block {block, fill} */
+    __shared__ uint4 tab[64];   /* per tile, this batch: {run start, codes into the open block, the open block, first new block} */
+    __shared__ uint32_t tfill[64]; /* ... and the open block's fill before the batch */
+    const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
+    const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
+    const uint64_t nbatch = (n + kBinBatch - 1) / kBinBatch;
+    if (threadIdx.x < 64) info[threadIdx.x] = make_uint2(kNoBlk, BP);
+    const uint32_t shift = 10 + FMGI_TILE_BITS;
+    typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+    for (uint64_t b = blockIdx.x; b < nbatch; b += gridDim.x) {
+        /* the wave's kBinPer * 64 codes (n is a multiple of FMGI_STREAM_BLOCK: a wave's part is all in or out) */
+        const uint64_t w0 = b * kBinBatch + (uint64_t)wave * (kBinPer * 64);
+        uint32_t c[kBinPer];
+        if (w0 < n) {
+            const __attribute__((address_space(1))) u32x4 *src = (const __attribute__((address_space(1))) u32x4 *)(dense + w0);
+#pragma unroll
+            for (int u = 0; u < kBinPer / 4; u++) {
+                const u32x4 q = src[64 * u + lane];
+                c[4 * u] = q.x, c[4 * u + 1] = q.y, c[4 * u + 2] = q.z, c[4 * u + 3] = q.w;
+            }
+        } else {
+#pragma unroll
+            for (int e = 0; e < kBinPer; e++) c[e] = kSentinel;
+        }
+#pragma unroll
+        for (int e = 0; e < kBinPer; e++) /* a tile past P is never written by the bake: treated as a sentinel */
+            if (c[e] != kSentinel && (c[e] >> shift) >= (uint32_t)P) c[e] = kSentinel;
+        hist[wave][lane] = 0;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int e = 0; e < kBinPer; e++)
+            if (c[e] != kSentinel) atomicAdd(&hist[wave][c[e] >> shift], 1u);
+        __syncthreads();
+        /* lane group (tile t = tid / 16, wave w = tid % 16): exclusive prefix over the waves of tile t */
+        const int st = threadIdx.x >> 4, sw = threadIdx.x & 15;
+        const uint32_t v = hist[sw][st];
+        uint32_t incl = v;
+#pragma unroll
+        for (int off = 1; off < 16; off <<= 1) {
+            const uint32_t o = __shfl_up(incl, off, 16);
+            if (sw >= off) incl += o;
+        }
+        if (sw == 15) ttot[st] = incl;
+        __syncthreads();
+        if (wave == 0) { /* tiles' run starts: an exclusive scan of the 64 tile totals */
+            const uint32_t x = lane < P ? ttot[lane] : 0u;
+            uint32_t in2 = x;
+#pragma unroll
+            for (int off = 1; off < 64; off <<= 1) {
+                const uint32_t o = __shfl_up(in2, off, 64);
+                if (lane >= off) in2 += o;
+            }
+            tstart[lane] = in2 - x;
+        }
+        __syncthreads();
+        hist[sw][st] = tstart[st] + incl - v; /* the wave's cursor in tile st's run */
+        __syncthreads();
+#pragma unroll
+        for (int e = 0; e < kBinPer; e += 4) {
+            uint32_t o[4];
+#pragma unroll
+            for (int k = 0; k < 4; k++) o[k] = c[e + k] != kSentinel ? atomicAdd(&hist[wave][c[e + k] >> shift], 1u) : 0u;
+#pragma unroll
+            for (int k = 0; k < 4; k++)
+                if (c[e + k] != kSentinel) stage[o[k]] = c[e + k];
+        }
+        __syncthreads();
+        if (wave == 0) { /* (after the scatter: no code is held in registers) */
+            const uint32_t x = lane < P ? ttot[lane] : 0u;
+            if (lane < P && x) { /* the tile's run into its open block, then whole new blocks */
+                const uint2 inf = info[lane];
+                const uint32_t room = inf.x == kNoBlk ? 0u : BP - inf.y;
+                const uint32_t first = x < room ? x : room, rest = x - first;
+                const uint32_t nnew = (rest + BP - 1) / BP;
+                uint32_t b0 = kNoBlk;
+                if (nnew) {
+                    const unsigned long long nb = atomicAdd(pool_cursor, (unsigned long long)nnew);
+                    if (nb + nnew <= pool_blocks) {
+                        b0 = (uint32_t)nb;
+                        for (uint32_t j = 0; j < nnew; j++) {
+                            block_tile[b0 + j] = (uint32_t)lane;
+                            block_len[b0 + j] = BP; /* every block but the tile's last is full; the last is set
+                                                      when the workgroup closes it */
+                        }
+                    } else { /* (never, by sizing) blocks past the pool: recorded empty, codes sent to atomics */
+                        for (uint64_t j = nb; j < pool_blocks && j < nb + nnew; j++) {
+                            block_tile[j] = 0u;
+                            block_len[j] = 0u;
+                        }
+                    }
+                }
+                tab[lane] = make_uint4(tstart[lane], first, inf.x, b0);
+                tfill[lane] = inf.y;
+                if (nnew) info[lane] = make_uint2(b0, b0 == kNoBlk ? 0u : rest - (nnew - 1) * BP);
+                else info[lane] = make_uint2(inf.x, inf.y + x);
+            }
+        }
+        __syncthreads();
+        const uint32_t total = tstart[63]; /* (P <= 63: tile 63 is empty) */
+        for (uint32_t i = threadIdx.x; i < total; i += kBinThreads) {
+            const uint32_t code = stage[i];
+            const uint4 tb = tab[code >> shift];
+            const uint32_t k = i - tb.x;
+            if (k < tb.y) {
+                pool[(uint64_t)tb.z * BP + tfill[code >> shift] + k] = code;
+            } else if (tb.w != kNoBlk) {
+                const uint32_t r = k - tb.y;
+                pool[(uint64_t)(tb.w + r / BP) * BP + (r % BP)] = code;
+            } else {
+                bin_atomic(colpack, lm, code);
+            }
+        }
+        __syncthreads();
+    }
+    /* the workgroup's open blocks: their lengths (a full one was recorded when it was taken) */
+    if (threadIdx.x < 64 && (int)threadIdx.x < P) {
+        const uint2 inf = info[threadIdx.x];
+        if (inf.x != kNoBlk) block_len[inf.x] = inf.y;
+    }
+}
+
 } // namespace
 
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s) {
     const int P = (num_texels + kTileTexels - 1) / kTileTexels;
     const size_t plds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16;
-    if (sb.presort == 2) {
+    if (sb.presort == 3) { /* the dense stream: binned into the pool, then folded as the bucket layout */
+        hipError_t e = fmgi_set_lds_attr_once<6>((const void *)k_bin, kBinBatch * 4);
+        if (e != hipSuccess) return e;
+        hipLaunchKernelGGL(k_bin, dim3((unsigned)std::max(1, sb.bin_grid)), dim3(kBinThreads), (size_t)kBinBatch * 4, s,
+                           sb.dense, sb.cursor + 1, sb.dense_cap, P, sb.stream, sb.block_tile, sb.block_len, sb.cursor,
+                           sb.pool_blocks, (const uint4 *)sb.colpack, lm);
+        e = hipGetLastError();
+        if (e != hipSuccess) return e;
+    }
+    if (sb.presort >= 2) {
         /* the blocks listed by tile (counts, then each workgroup's range in its tiles' parts), then the sums */
         const unsigned lg = (unsigned)((sb.pool_blocks + (uint64_t)kListThreads * kListPerThread - 1) /
                                        ((uint64_t)kListThreads * kListPerThread));

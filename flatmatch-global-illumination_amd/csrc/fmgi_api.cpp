@@ -875,7 +875,16 @@ static uint64_t stream_cap_for(uint64_t items, int grid, int block) {
 
 /* STREAM layouts (BakeArgs::presort): 0 = unsorted codes, folded through k_slice_sort's sorted copy;
    1 = ring-sized segments presorted by tile; 2 = per-wave tile buckets (bucket_out / k_bucket_fold) */
-enum { kStreamSliced = 0, kStreamSegments = 1, kStreamBuckets = 2 };
+enum { kStreamSliced = 0, kStreamSegments = 1, kStreamBuckets = 2, kStreamDense = 3 };
+
+/* the dense stream of a chunk (kStreamDense): one code or sentinel per lane and loop iteration. An item
+   scans at most 900 times (8 deposits and one escape per photon); a lane idles (sentinels) at most while
+   the other lanes of its wave finish an item each; plus each wave's last partly written block */
+static uint64_t dense_cap_for(uint64_t items, int grid, int block) {
+    const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
+    return items * (FMGI_EVENTS_PER_ITEM + FMGI_PHOTONS_PER_ITEM) +
+           waves * (64ull * (FMGI_EVENTS_PER_ITEM + FMGI_PHOTONS_PER_ITEM) + 2 * FMGI_STREAM_BLOCK);
+}
 
 /* the bucketed stream's pool, in blocks: every code of the chunk, plus one partly filled bucket per wave
    and tile */
@@ -888,13 +897,14 @@ static uint64_t bucket_pool_blocks(uint64_t cap, int P, int grid, int block) {
     return (cap + pads + FMGI_BUCKET_BLOCK - 1) / FMGI_BUCKET_BLOCK + waves * (uint64_t)(P + FMGI_BUCKET_ALLOC) + 8;
 }
 static uint64_t stream_alloc_codes(uint64_t cap, int P, int grid, int block, int mode) {
-    return mode == kStreamBuckets ? bucket_pool_blocks(cap, P, grid, block) * FMGI_BUCKET_BLOCK : cap;
+    return mode >= kStreamBuckets ? bucket_pool_blocks(cap, P, grid, block) * FMGI_BUCKET_BLOCK : cap;
 }
 
 static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
     return stream_alloc_codes(stream_cap_for(items, grid, block), P, grid, block, mode) > c->sb_cap_alloc[k] ||
-           (mode == kStreamSliced && !c->sb[k].sorted);
+           (mode == kStreamSliced && !c->sb[k].sorted) ||
+           (mode == kStreamDense && dense_cap_for(items, grid, block) > c->sb[k].dense_alloc);
 }
 
 static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
@@ -912,10 +922,23 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         c->sb_cap_alloc[k] = codes;
     }
     sb.presort = mode;
+    sb.dense_cap = 0;
+    if (mode == kStreamDense) { /* the bake's dense stream beside the pool k_bin fills */
+        const uint64_t dcap = dense_cap_for(items, grid, block);
+        if (dcap > sb.dense_alloc) {
+            hipFree(sb.dense);
+            sb.dense = nullptr;
+            sb.dense_alloc = 0;
+            HIPCHK(hipMalloc(&sb.dense, dcap * sizeof(uint32_t)));
+            sb.dense_alloc = dcap;
+        }
+        sb.dense_cap = dcap;
+        sb.bin_grid = 2 * std::max(1, c->num_cus);
+    }
     /* run tables: per 8192-code slice (sorted by k_slice_sort), or per ring-sized segment (presorted); the
        bucketed stream's per-block tile, length and list instead */
     uint64_t entries = 0;
-    if (mode == kStreamBuckets) {
+    if (mode >= kStreamBuckets) {
         sb.pool_blocks = bucket_pool_blocks(cap, P, grid, block);
         /* FMGI_POOL_LIMIT=n (tests): at most n pool blocks, so the bake runs out of them and takes the
            exact atomic fallback (bucket_atomic) for the rest of its codes */
@@ -935,9 +958,9 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         HIPCHK(hipMalloc(&sb.toff, entries * sizeof(uint16_t)));
         c->sb_entries_alloc[k] = entries;
     }
-    sb.block_tile = mode == kStreamBuckets ? (uint32_t *)sb.toff : nullptr;
-    sb.block_len = mode == kStreamBuckets ? sb.block_tile + sb.pool_blocks : nullptr;
-    sb.block_list = mode == kStreamBuckets ? sb.block_len + sb.pool_blocks : nullptr;
+    sb.block_tile = mode >= kStreamBuckets ? (uint32_t *)sb.toff : nullptr;
+    sb.block_len = mode >= kStreamBuckets ? sb.block_tile + sb.pool_blocks : nullptr;
+    sb.block_list = mode >= kStreamBuckets ? sb.block_len + sb.pool_blocks : nullptr;
     if (!sb.cursor) HIPCHK(hipMalloc(&sb.cursor, 64));
     sb.cap = cap;
     sb.colpack = c->d_colpack;
@@ -952,7 +975,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
            per-workgroup set-up and flush) */
         /* slice-sorted (lightmaps of more than 63 tiles): ~48 rounds (30-room layout, 358 tiles: fold 7.49 /
            7.31 / 6.34 / 5.97 ms at 8 / 4 / 16 / 32 groups per tile, profiles/r03/s33) */
-        const int rounds = mode == kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 48);
+        const int rounds = mode >= kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 48);
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
@@ -960,7 +983,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         if (!(ge && atoi(ge) > 0)) {
             if (mode == kStreamSegments)
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 1024));
-            if (mode == kStreamBuckets) /* at least one 4-KB block per wave of every workgroup */
+            if (mode >= kStreamBuckets) /* at least one 4-KB block per wave of every workgroup */
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
                                                     std::max<uint64_t>(8, (cap / FMGI_BUCKET_BLOCK) / ((uint64_t)P * 16)));
             if (mode == kStreamSliced) /* at least one big slice's worth of codes per workgroup and tile */
@@ -982,6 +1005,9 @@ static void release_stream_buffers(fmgi_context *c) {
         (void)hipFree(c->sb[k].stream);
         (void)hipFree(c->sb[k].sorted);
         (void)hipFree(c->sb[k].toff);
+        (void)hipFree(c->sb[k].dense);
+        c->sb[k].dense = nullptr;
+        c->sb[k].dense_alloc = 0;
         c->sb[k].stream = c->sb[k].sorted = nullptr;
         c->sb[k].toff = nullptr;
         c->sb_cap_alloc[k] = 0;
@@ -1114,7 +1140,9 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
            vs 3.65e9 photons/s FAST, 3.02e9 GRID) when the floor/ceiling records share few planes */
         if (c->auto_kernel == FMGI_KERNEL_FAST && 4 * gb.J[2] < fb.J[2]) c->auto_kernel = FMGI_KERNEL_HYBRID;
         /* the largest LDS use (STREAM rings) decides, so the choice holds for every accumulation mode */
-        c->auto_kernel = fitting_kernel(c, c->auto_kernel, FMGI_ACCUM_STREAM, bake_block());
+        const char *se = getenv("FMGI_SCATTER");
+        c->auto_kernel = fitting_kernel(c, c->auto_kernel, (se && atoi(se) == 1) ? kAccScatter : FMGI_ACCUM_STREAM,
+                                        bake_block());
     }
     if (c->device != FMGI_HOST_ONLY) {
     HIPCHK(hipSetDevice(c->device));
@@ -1374,7 +1402,13 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
        lanes) left SIMDs unevenly loaded (box200: 149.6 ms against 123.8 ms at 256, profiles/r03/s3) */
     /* (768-lane workgroups measured pathological for every instance built for 4 waves/SIMD: box200 bake
        1.6-2.2 s instead of 0.05-0.08 s, profiles/r04/s7; not offered) */
-    const int blocks_all[] = {256, 512, 1024};
+    /* AccScatter (no rings: ~0.4 KB of LDS per wave) is built for 6 waves/SIMD: 768-lane workgroups, two per
+       CU, keep the grid cells staged beside the walls at 24 waves per CU, which 512-lane ones (three per CU)
+       cannot */
+    const int blocks_ring[] = {256, 512, 1024}, blocks_scatter[] = {256, 512, 768, 1024};
+    const bool scat = accum == kAccScatter;
+    const int *blocks_all = scat ? blocks_scatter : blocks_ring;
+    const int nblocks = scat ? 4 : 3;
     /* the grid cells in LDS: every cell lookup an LDS read instead of an L2 one. The closed boxes' coarse
        grid asks for it (kept only if the wave count holds); FMGI_CELLS_LDS=1 forces it for any grid or
        hybrid scan that fits, 0 turns it off (experiments) */
@@ -1386,7 +1420,8 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
         bb = p.block;
         bw = waves(p.block, bytes);
         if (forced_block) return;
-        for (int B : blocks_all) {
+        for (int k = 0; k < nblocks; k++) {
+            const int B = blocks_all[k];
             const int w = waves(B, bytes);
             if (w > bw) { bw = w; bb = B; }
         }
@@ -1467,8 +1502,9 @@ static uint64_t stream_chunk_items(fmgi_context *c, int sets, int mode) {
     /* the stream, and the slice-sorted copy of the unsorted layout (buckets: the pool is the stream plus its
        pads (<= 3 * 63 per 1024 codes), one partly filled block per wave and tile, and the block tables,
        within the 25 % allowance) */
-    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamBuckets ? 1.25 : 1.0);
-    const double held = 4.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]) * (c->sb[0].sorted ? 2.0 : 1.0);
+    const double copies = mode == kStreamSliced ? 2.0 : (mode == kStreamBuckets ? 1.25 : (mode == kStreamDense ? 2.5 : 1.0));
+    const double held = 4.0 * (double)(c->sb_cap_alloc[0] + c->sb_cap_alloc[1]) * (c->sb[0].sorted ? 2.0 : 1.0) +
+                        4.0 * (double)(c->sb[0].dense_alloc + c->sb[1].dense_alloc);
     const double avail = (double)fr + held;
     uint64_t items = (uint64_t)(avail * 0.5 / ((double)sets * copies * 4.0 * FMGI_EVENTS_PER_ITEM));
     /* slices are indexed in 32 bits by the sort kernel's grid */
@@ -1487,15 +1523,22 @@ static int stream_layout(const fmgi_context *c) {
     int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamBuckets : kStreamSliced;
     if (pre_env && P >= 1 && P <= FMGI_PRESORT_MAX_TILES) smode = std::max(0, std::min(2, atoi(pre_env)));
     if (pre_env && atoi(pre_env) == 0) smode = kStreamSliced;
+    if (smode == kStreamBuckets) { /* FMGI_DENSE=1: the dense stream and k_bin instead of the bake's rings */
+        const char *de = getenv("FMGI_DENSE");
+        if (de && atoi(de) == 1) smode = kStreamDense;
+    }
     return smode;
 }
 
 /* the accumulation of a bake's kernel instance: the bucket layout of the stream through per-wave rings
    (kAccBucket) or through per-workgroup tile lines (kAccLines, FMGI_LINES=1) */
 static int exec_accum(const fmgi_context *c) {
+    if (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamDense) return kAccDense;
     if (c->accum != FMGI_ACCUM_STREAM || stream_layout(c) != kStreamBuckets) return c->accum;
     const char *le = getenv("FMGI_LINES");
-    return (le && atoi(le) == 1) ? kAccLines : kAccBucket;
+    if (le && atoi(le) == 1) return kAccLines;
+    const char *se = getenv("FMGI_SCATTER");
+    return (se && atoi(se) == 1) ? kAccScatter : kAccBucket;
 }
 
 static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
@@ -1510,13 +1553,14 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     /* the kernel instance's accumulation: the bucket layout of the stream has its own (kAccBucket) */
     const int kacc = exec_accum(c);
     if (was_auto) kernel = c->auto_kernel;
-    kernel = fitting_kernel(c, kernel, c->accum, bake_block()); /* an image too large for LDS: same results, other scan */
+    /* an image too large for LDS: same results, other scan (checked with the LDS of the instance launched) */
+    kernel = fitting_kernel(c, kernel, kacc, bake_block());
     if (b == e) return FMGI_OK;
     /* a launch with at most half as many items as resident lanes runs ScanFast with cooperative lanes
        (below): on such launches that beats the hybrid scan's single lane per item (config 1: 6.6 ms
        hybrid bake vs ~3.5 ms cooperative) */
     if (was_auto && kernel == FMGI_KERNEL_HYBRID && !trace && c->accum == FMGI_ACCUM_STREAM &&
-        fitting_kernel(c, FMGI_KERNEL_FAST, c->accum, bake_block()) == FMGI_KERNEL_FAST) {
+        fitting_kernel(c, FMGI_KERNEL_FAST, kacc, bake_block()) == FMGI_KERNEL_FAST) {
         const StagePlan fp = plan_stage(c, FMGI_KERNEL_FAST, kacc, trace);
         const uint64_t lanes_max =
             (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, kacc, trace, fp.block, fp.bytes, UINT64_MAX) * fp.block;
@@ -1837,10 +1881,19 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             a.pool_cursor = sb.cursor;
             a.pool_blocks = sb.pool_blocks;
         }
+        if (smode == kStreamDense) { /* the bake writes the dense stream; k_bin fills the pool */
+            a.stream = sb.dense;
+            a.stream_cap = sb.dense_cap;
+            a.stream_cursor = sb.cursor + 1;
+        }
         HIPCHK(fetch_table(cb, ce));
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
-        HIPCHK(hipMemsetAsync(sb.cursor, 0, 8, s));
+        HIPCHK(hipMemsetAsync(sb.cursor, 0, 16, s)); /* the pool / stream cursor and the dense stream's */
         hipEvent_t t0 = nullptr, t1 = nullptr;
+        if (getenv("FMGI_SHOW_LAUNCH")) /* experiments: the launch shape the planner chose */
+            fprintf(stderr, "fmgi: bake kernel %d accum %d block %d grid %d lds %zu (staged %d: rects %d srcs %d cells %d)\n",
+                    kernel_instance(c, kernel), kacc, block, grid, fmgi_bake_lds(kernel_instance(c, kernel), kacc, block, a.fimg_bytes, nullptr),
+                    a.fimg_bytes, a.rects_off, a.srcs_off, a.cells_off);
         HIPCHK(time_begin(c, s, t0));
         HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), kacc, trace, grid, block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));

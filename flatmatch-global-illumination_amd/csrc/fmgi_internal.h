@@ -195,6 +195,11 @@ struct StreamBufs {
     uint32_t *block_list;             /* [pool_blocks] block ids grouped by tile (the fold's list)     */
     uint32_t *tile_blocks;            /* [2 * (FMGI_PRESORT_MAX_TILES + 1)] counts, then list cursors  */
     uint64_t pool_blocks;
+    /* dense stream (presort == 3): the bake's codes in iteration order (dense_cap entries, reserved through
+       cursor[1]); k_bin moves them into the bucket pool (`stream`, pool cursor = cursor[0]) */
+    uint32_t *dense;
+    uint64_t dense_cap, dense_alloc;
+    int bin_grid;                     /* k_bin workgroups (persistent: two per CU)                     */
 };
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);
 
@@ -208,6 +213,9 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
    its own kernel instance) */
 constexpr int kAccBucket = 5;
 constexpr int kAccLines = 6; /* the bucket layout through per-workgroup tile lines (AccLines) */
+constexpr int kAccScatter = 7; /* the bucket layout stored lane by lane into per-wave tile blocks (AccScatter) */
+#define FMGI_SCATTER_STRIDE 128 /* AccScatter: LDS dwords per wave (64 x {fill, block} words) */
+constexpr int kAccDense = 8; /* a dense code stream (one code or sentinel per lane and iteration), binned by k_bin */
 /* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
    FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */
 #define FMGI_KVAR_AXES 0x100

@@ -1618,9 +1618,197 @@ struct AccLines {
     }
 };
 
+/*
+ * The bucket layout written straight from the lanes (kAccScatter). The rings of AccStreamT cost 6 KB of LDS
+ * per wave and a flush that holds 16 codes per lane while it sorts them (115 VGPRs): the bake ran at 4 waves
+ * per SIMD, where tracing alone takes 64 ms on box200 against 49 ms at 6 (profiles/r04/s3). Here nothing is
+ * staged: a wave keeps, per fold tile t, one open FMGI_BUCKET_BLOCK-code block of the pool and its fill in a
+ * 64-bit LDS word tab[t] = {fill, block} (512 B per wave). A depositing lane takes its slot with one
+ * ds_add_rtn_u64 on its tile's word (the lanes of one tile get consecutive ranks) and stores its code at
+ * pool[block * BP + rank] with a plain dword store. The rank that reaches BP (rare: ~every 16 iterations per
+ * wave) closes the block, takes the next one from the wave's reserved batch (one pool-cursor atomic per
+ * FMGI_BUCKET_ALLOC blocks) and resets the word to {ranks past BP, new block}; the lanes past BP store into
+ * the new block. A bucket's codes are the prefix [0, fill) of each block, so the blocks are exactly the
+ * bucketed layout k_bucket_fold reads (no sentinel pads). The stores land 4 B at a time in ~46 open lines
+ * per wave; L2 merges them (write-back, byte masks), so HBM sees whole lines in the common case.
+ */
+struct AccScatter {
+    typedef unsigned long long u64;
+    static constexpr uint32_t BP = FMGI_BUCKET_BLOCK, kNoBlock = 0xFFFFFFFFu;
+    static constexpr int kFree = 63; /* tab[kFree] = the wave's reserved pool blocks {first, count} */
+    static constexpr uint32_t kAllocBatch = FMGI_BUCKET_ALLOC;
+    static __device__ __forceinline__ int layout(const BakeArgs &) { return 2; }
+    static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
+    static __device__ __forceinline__ u64 *tab(uint32_t *base) { return (u64 *)base; }
+
+    static __device__ __forceinline__ void init(const BakeArgs &, uint32_t *base) {
+        const uint32_t l = __lane_id();
+        /* {fill = BP, no block}: a tile's first code opens its first block */
+        tab(base)[l] = l == (uint32_t)kFree ? 0ull : (((u64)kNoBlock << 32) | BP);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    }
+
+    /* a fresh pool block for tile t on every live lane with `need` (kNoBlock if the pool is exhausted: never,
+       by sizing). Called where every live lane of the wave is active. */
+    static __device__ __forceinline__ uint32_t alloc(const BakeArgs &a, u64 *T, bool need, uint32_t t) {
+        const uint64_t m = __ballot(need);
+        const uint32_t n = (uint32_t)__popcll(m);
+        const uint32_t rk = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const u64 fl = T[kFree];
+        const uint32_t first = (uint32_t)fl, cnt = (uint32_t)(fl >> 32);
+        uint32_t b = need && rk < cnt ? first + rk : kNoBlock;
+        uint32_t nfirst = first + n, ncnt = cnt - n;
+        if (cnt < n) { /* (uniform) the rest of the batch, then a new batch */
+            const uint32_t more = n - cnt, want = more > kAllocBatch ? more : kAllocBatch;
+            const uint64_t live = __ballot(true);
+            const int leader = __ffsll((long long)live) - 1;
+            unsigned long long nb = 0;
+            if ((int)__lane_id() == leader) nb = atomicAdd(a.pool_cursor, (unsigned long long)want);
+            nb = __shfl(nb, leader, 64);
+            const uint64_t have64 = nb < a.pool_blocks ? a.pool_blocks - nb : 0ull;
+            const uint32_t have = (uint32_t)(have64 < want ? have64 : want);
+            if (need && rk >= cnt && rk - cnt < have) b = (uint32_t)nb + (rk - cnt);
+            const uint32_t used = more < have ? more : have;
+            nfirst = have ? (uint32_t)nb + used : 0u;
+            ncnt = have - used;
+        }
+        if (b != kNoBlock) a.block_tile[b] = t;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if ((int)__lane_id() == __ffsll((long long)__ballot(true)) - 1) T[kFree] = ((u64)ncnt << 32) | nfirst;
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        return b;
+    }
+
+    static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &, uint32_t *base, bool dep,
+                                                  uint32_t code) {
+        u64 *T = tab(base);
+        const uint32_t t = code >> (10 + FMGI_TILE_BITS);
+        u64 old = 0;
+        if (dep) old = __hip_atomic_fetch_add(T + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        uint32_t rank = (uint32_t)old, blk = (uint32_t)(old >> 32);
+        const bool full = dep && rank >= BP;
+        if (__ballot(full)) { /* (uniform, rare) a block of some tile filled up */
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            const bool opener = full && rank == BP; /* one lane per filled tile */
+            const uint32_t now = opener ? (uint32_t)T[t] : 0u; /* the fill after every lane's add */
+            if (opener && blk != kNoBlock) a.block_len[blk] = BP;
+            const uint32_t nb = alloc(a, T, opener, t);
+            if (opener) T[t] = ((u64)nb << 32) | (now - BP);
+            __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            if (full) {
+                blk = (uint32_t)(T[t] >> 32);
+                rank -= BP;
+            }
+        }
+#ifdef FMGI_SCATTER_EXP /* PROFILING ONLY: 1 = the slot is taken but the code is not stored (lightmap lost) */
+        if (FMGI_SCATTER_EXP == 1 && code != 0xFFFFFFFEu) return;
+#endif
+        if (dep) {
+            if (blk != kNoBlock) ((__attribute__((address_space(1))) uint32_t *)a.stream)[(uint64_t)blk * BP + rank] = code;
+            else AccBucket::bucket_atomic(a, code);
+        }
+    }
+
+    /* after the loop (every lane of the wave reconverged): the open blocks' lengths, and the reserved blocks
+       that were never handed out recorded empty */
+    static __device__ __forceinline__ void finish(const BakeArgs &a, WaveStream &, uint32_t *base) {
+        const u64 *T = tab(base);
+        const uint32_t l = __lane_id();
+        if ((int)l < a.ntiles) {
+            const u64 v = T[l];
+            const uint32_t blk = (uint32_t)(v >> 32), fill = (uint32_t)v;
+            if (blk != kNoBlock) a.block_len[blk] = fill < BP ? fill : BP;
+        }
+        const u64 fl = T[kFree];
+        const uint32_t first = (uint32_t)fl, cnt = (uint32_t)(fl >> 32);
+        for (uint32_t k = l; k < cnt; k += 64) {
+            a.block_tile[first + k] = 0u;
+            a.block_len[first + k] = 0u;
+        }
+    }
+};
+
+/*
+ * The dense stream (kAccDense): the bake only writes, the fold's binning pass (k_bin, fmgi_accum.hip) sorts.
+ * At the end of every iteration the depositing lanes of a wave take consecutive slots (ballot + mbcnt) after
+ * the wave's running count in its current FMGI_STREAM_BLOCK-code block and store their codes there: one
+ * coalesced store of <= 256 B per wave and iteration, no LDS, and as state only the block base and the count
+ * (both wave-uniform). A full block is followed by the next one (one cursor atomic per 4096 codes); an
+ * iteration whose codes straddle the end splits them over the two. After the loop the rest of the wave's last
+ * block is filled with sentinels, so every reserved block is entirely written.
+ */
+struct AccDense {
+    static constexpr uint32_t kSent = 0xFFFFFFFFu, BLK = FMGI_STREAM_BLOCK;
+    static __device__ __forceinline__ int layout(const BakeArgs &) { return 3; }
+    static __device__ __forceinline__ void deposit(const BakeArgs &, int, int, f3) {}
+    static __device__ __forceinline__ void init(const BakeArgs &, uint32_t *) {}
+    static __device__ __forceinline__ uint32_t sgpr(uint32_t v) { return __builtin_amdgcn_readfirstlane(v); }
+    static __device__ __forceinline__ uint64_t sgpr64(uint64_t v) {
+        return ((uint64_t)sgpr((uint32_t)(v >> 32)) << 32) | sgpr((uint32_t)v);
+    }
+    /* ws.base: the wave's current block, ws.tot: the room left in it (0 at the start: no block); uniform
+       over the live lanes, kept in SGPRs. Called where every live lane of the wave is active. */
+    static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &ws, uint32_t *, bool dep,
+                                                  uint32_t code) {
+        const uint64_t m = __ballot(dep);
+        if (m == 0) return;
+        const uint32_t n = (uint32_t)__popcll(m);
+        const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+        const uint32_t room = sgpr(ws.tot);
+        const uint64_t base = sgpr64(ws.base);
+        uint64_t dst = base + (BLK - room) + r;
+        if (n > room) { /* (uniform) the block fills: the rest of the codes start the next one */
+            unsigned long long nb = 0;
+            if (r == 0) { /* (the first depositing lane) */
+                nb = atomicAdd(a.stream_cursor, (unsigned long long)BLK);
+                if (nb + BLK > a.stream_cap) atomicAdd(a.overflow, 1ull);
+            }
+            nb = sgpr64(__shfl(nb, __ffsll((long long)m) - 1, 64));
+            if (r >= room) dst = nb + (r - room);
+            ws.base = nb;
+            ws.tot = BLK - (n - room);
+        } else {
+            ws.tot = room - n;
+        }
+        /* (a reservation past the end, never by sizing, is counted and its codes dropped: the call fails) */
+        if (dep && dst < a.stream_cap) ((__attribute__((address_space(1))) uint32_t *)a.stream)[dst] = code;
+    }
+    /* after the loop (every lane of the wave reconverged): the state of the lane that appended last (the
+       wave's blocks are reserved in increasing order, so it has the largest base + codes in the block), then
+       sentinels in the rest of its block */
+    static __device__ __forceinline__ void finish(const BakeArgs &a, WaveStream &ws, uint32_t *) {
+        const uint64_t key = ws.tot || ws.base ? ws.base + (BLK - ws.tot) + 1 : 0ull;
+        uint64_t mx = key;
+        for (int off = 32; off > 0; off >>= 1) {
+            const uint64_t o = __shfl_xor(mx, off, 64);
+            mx = o > mx ? o : mx;
+        }
+        if (mx == 0) return; /* the wave appended nothing */
+        const int src = __ffsll((long long)__ballot(key == mx)) - 1;
+        const uint64_t base = __shfl(ws.base, src, 64);
+        const uint32_t room = __shfl(ws.tot, src, 64);
+        for (uint32_t k = BLK - room + __lane_id(); k < BLK; k += 64)
+            if (base + k < a.stream_cap) ((__attribute__((address_space(1))) uint32_t *)a.stream)[base + k] = kSent;
+    }
+};
+
 template <class Acc>
 struct HasAppend {
     static constexpr bool value = false;
+};
+template <>
+struct HasAppend<AccDense> {
+    static constexpr bool value = true;
+};
+
+template <>
+struct HasAppend<AccScatter> {
+    static constexpr bool value = true;
 };
 template <int Mode>
 struct HasAppend<AccStreamT<Mode>> {
@@ -1643,6 +1831,10 @@ __device__ __forceinline__ uint32_t *acc_region<AccBucket>(char *lds, const Bake
 template <>
 __device__ __forceinline__ uint32_t *acc_region<AccLines>(char *lds, const BakeArgs &a) {
     return (uint32_t *)(lds + a.ring_off);
+}
+template <>
+__device__ __forceinline__ uint32_t *acc_region<AccScatter>(char *lds, const BakeArgs &a) {
+    return (uint32_t *)(lds + a.ring_off) + (threadIdx.x >> 6) * FMGI_SCATTER_STRIDE;
 }
 
 /* ---- the per-lane photon state machine ------------------------------------------------------- */
@@ -1714,6 +1906,13 @@ template <class Acc>
 constexpr int acc_min_waves() { return 1; }
 template <>
 constexpr int acc_min_waves<AccLines>() { return 6; }
+#ifndef FMGI_SCATTER_WAVES /* AccScatter: the registers of this many waves per SIMD (experiment builds: 4, 5, 6) */
+#define FMGI_SCATTER_WAVES 6
+#endif
+template <>
+constexpr int acc_min_waves<AccScatter>() { return FMGI_SCATTER_WAVES; }
+template <>
+constexpr int acc_min_waves<AccDense>() { return FMGI_SCATTER_WAVES; }
 template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
@@ -2092,6 +2291,8 @@ const void *kernel_acc(int accum, bool trace) {
     if (accum == 4) return kernel_ptr<Scan, AccStream>(trace);
     if (accum == kAccBucket) return kernel_ptr<Scan, AccBucket>(trace);
     if (accum == kAccLines) return kernel_ptr<Scan, AccLines>(trace);
+    if (accum == kAccScatter) return kernel_ptr<Scan, AccScatter>(trace);
+    if (accum == kAccDense) return kernel_ptr<Scan, AccDense>(trace);
     return kernel_ptr<Scan, AccFx3>(trace);
 }
 
@@ -2102,14 +2303,18 @@ void launch_acc(const BakeArgs &a, int accum, bool trace, dim3 grid, dim3 block,
     else if (accum == 4) launch3<Scan, AccStream>(a, trace, grid, block, lds, s);
     else if (accum == kAccBucket) launch3<Scan, AccBucket>(a, trace, grid, block, lds, s);
     else if (accum == kAccLines) launch3<Scan, AccLines>(a, trace, grid, block, lds, s);
+    else if (accum == kAccScatter) launch3<Scan, AccScatter>(a, trace, grid, block, lds, s);
+    else if (accum == kAccDense) launch3<Scan, AccDense>(a, trace, grid, block, lds, s);
     else launch3<Scan, AccFx3>(a, trace, grid, block, lds, s);
 }
 
 const void *bake_kernel(int kernel, int accum, bool trace) {
     if (kernel == FMGI_KERNEL_FAST_COOP)
         return accum == kAccBucket ? kernel_ptr<ScanFastCoop, AccBucket>(false)
-                                   : (accum == kAccLines ? kernel_ptr<ScanFastCoop, AccLines>(false)
-                                                         : kernel_ptr<ScanFastCoop, AccStream>(false));
+               : accum == kAccLines ? kernel_ptr<ScanFastCoop, AccLines>(false)
+               : accum == kAccScatter ? kernel_ptr<ScanFastCoop, AccScatter>(false)
+               : accum == kAccDense ? kernel_ptr<ScanFastCoop, AccDense>(false)
+                                    : kernel_ptr<ScanFastCoop, AccStream>(false);
     if (kernel == (2 | FMGI_KVAR_AXES)) return kernel_acc<ScanGridAxes>(accum, trace);
     if (kernel == (4 | FMGI_KVAR_PLAN)) return kernel_acc<ScanHybridPlan>(accum, trace);
     kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN);
@@ -2129,6 +2334,7 @@ size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
     if (accum == kAccLines) return img + (size_t)FMGI_LINES_DWORDS * 4;
+    if (accum == kAccScatter) return img + (size_t)(block / 64) * FMGI_SCATTER_STRIDE * 4;
     if (accum == kAccBucket) return img + (size_t)(block / 64) * FMGI_RING_STRIDE_BUCKET * 4;
     return img + (accum == 4 ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
@@ -2170,8 +2376,12 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         if (e != hipSuccess) return e;
     }
     if (kernel == FMGI_KERNEL_FAST_COOP) {
-        if ((accum != 4 && accum != kAccBucket && accum != kAccLines) || trace) return hipErrorInvalidValue;
+        if ((accum != 4 && accum != kAccBucket && accum != kAccLines && accum != kAccScatter && accum != kAccDense) ||
+            trace)
+            return hipErrorInvalidValue;
         if (accum == kAccBucket) launch3<ScanFastCoop, AccBucket>(a, false, grid, blk, lds, s);
+        else if (accum == kAccScatter) launch3<ScanFastCoop, AccScatter>(a, false, grid, blk, lds, s);
+        else if (accum == kAccDense) launch3<ScanFastCoop, AccDense>(a, false, grid, blk, lds, s);
         else if (accum == kAccLines) launch3<ScanFastCoop, AccLines>(a, false, grid, blk, lds, s);
         else launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
     } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */

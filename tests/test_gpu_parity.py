@@ -171,15 +171,31 @@ def test_lightmap_box_prefix_exact(torch_cuda, box200, box2000, offsets, kernel,
         ctx.close()
 
 
-@pytest.mark.parametrize("presort,packed", [("2", None), ("1", None), ("0", "0"), ("0", "1")])
-def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, presort, packed):
-    """The STREAM fold from the bake's per-tile buckets (FMGI_PRESORT=2, the default for lightmaps of at
-    most 63 fold tiles), from the bake-side presorted segments (1) and from the slice-sorted stream (0;
-    its runs summed one at a time, or packed 16 slices to a wave as for lightmaps of more than 128 tiles)
-    give the oracle's lightmap, for full-ring flushes and for the partial rings at the end of a launch."""
-    os.environ["FMGI_PRESORT"] = presort
-    if packed is not None:
-        os.environ["FMGI_PACKED_RUNS"] = packed
+FOLD_LAYOUTS = {  # stream layout -> the environment that selects it
+    "buckets_ring": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "0", "FMGI_DENSE": "0"},
+    "buckets_scatter": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_DENSE": "0"},
+    "dense_bin": {"FMGI_PRESORT": "2", "FMGI_DENSE": "1"},
+    "presorted": {"FMGI_PRESORT": "1"},
+    "sliced": {"FMGI_PRESORT": "0", "FMGI_PACKED_RUNS": "0"},
+    "sliced_packed": {"FMGI_PRESORT": "0", "FMGI_PACKED_RUNS": "1"},
+}
+FOLD_ENV = sorted({k for v in FOLD_LAYOUTS.values() for k in v} | {"FMGI_POOL_LIMIT", "FMGI_CHUNK_ITEMS"})
+
+
+def _set_layout(name):
+    for k in FOLD_ENV:
+        os.environ.pop(k, None)
+    os.environ.update(FOLD_LAYOUTS[name])
+
+
+@pytest.mark.parametrize("layout", sorted(FOLD_LAYOUTS))
+def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, layout):
+    """Every STREAM layout gives the oracle's lightmap: per-tile buckets (the default for lightmaps of at most
+    63 fold tiles) filled through the bake's per-wave LDS rings (buckets_ring) or lane by lane (buckets_scatter),
+    the bake's dense code stream binned into buckets by k_bin (dense_bin), the bake-side presorted segments, and
+    the slice-sorted stream (its runs summed one at a time, or packed 16 slices to a wave as for lightmaps of more
+    than 128 tiles); for full-ring flushes and the partial rings / blocks at the end of a launch."""
+    _set_layout(layout)
     try:
         for sc, spa, lo, hi in ((box200, 172_413_793, 7_000, 27_000), (example_scene, 65_000, 0, 300)):
             L = _oracle_plan(sc, spa, offsets)
@@ -190,14 +206,16 @@ def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, pr
             assert ctx.stats()["stream_overflow"] == 0
             ctx.close()
     finally:
-        os.environ.pop("FMGI_PRESORT", None)
-        os.environ.pop("FMGI_PACKED_RUNS", None)
+        for k in FOLD_ENV:
+            os.environ.pop(k, None)
 
 
-def test_bucket_pool_exhaustion_falls_back_exactly(torch_cuda, box200, offsets):
-    """A bucketed stream whose pool runs out (FMGI_POOL_LIMIT caps it at 64 blocks, far fewer than the
-    bake needs) sends the rest of its codes through device atomics into the int64 lightmap
-    (AccStream::bucket_atomic): the lightmap still equals the oracle's."""
+@pytest.mark.parametrize("layout", ["buckets_ring", "buckets_scatter", "dense_bin"])
+def test_bucket_pool_exhaustion_falls_back_exactly(torch_cuda, box200, offsets, layout):
+    """A bucket pool that runs out (FMGI_POOL_LIMIT caps it at 64 blocks, far fewer than the bake needs) sends
+    the rest of the codes through device atomics into the int64 lightmap (the bake's bucket_atomic, k_bin's
+    bin_atomic), whichever way the buckets are filled: the lightmap still equals the oracle's."""
+    _set_layout(layout)
     os.environ["FMGI_POOL_LIMIT"] = "64"
     try:
         spa = 172_413_793
@@ -208,7 +226,8 @@ def test_bucket_pool_exhaustion_falls_back_exactly(torch_cuda, box200, offsets):
         assert np.array_equal(lm[:, :3], olm)
         ctx.close()
     finally:
-        os.environ.pop("FMGI_POOL_LIMIT", None)
+        for k in FOLD_ENV:
+            os.environ.pop(k, None)
 
 
 def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets):
