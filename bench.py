@@ -286,6 +286,14 @@ def binding_of(issue, atomic_rate):
                        % (100 * w["waiting"], 100 * w["issuing"], 100 * fr["valu"], 100 * fr["vmem"]))
 
 
+def weak_spa(cfg, world):
+    """numSamplesPerArea of a step on `world` GPUs: weak configs take spa x world (the reference's int
+    argument, global_illumination_cl.h:10), clamped to INT_MAX; the photons actually planned are what the
+    BENCH line reports (config.photons_per_step), and config.spa_clamped says when the clamp bit."""
+    spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
+    return min(spa, 2**31 - 1), spa > 2**31 - 1
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -336,8 +344,7 @@ def main():
         cfg["spa"] = args.spa
         cfg["desc"] += f" [spa overridden: {args.spa}]"
     sc = load_scene(cfg["scene"])
-    spa = cfg["spa"] * world if (cfg["weak"] and world > 1) else cfg["spa"]
-    spa = min(spa, 2**31 - 1)
+    spa, spa_clamped = weak_spa(cfg, world)
     kernel = {"auto": fmgi.KERNEL_AUTO, "grid": fmgi.KERNEL_GRID, "fast": fmgi.KERNEL_FAST,
               "exact": fmgi.KERNEL_EXACT, "hybrid": fmgi.KERNEL_HYBRID}[args.kernel]
 
@@ -398,16 +405,28 @@ def main():
         dist.barrier()
     elapsed = time.perf_counter() - t0
     st = ctx.stats()
+    # every rank's photon counter must cover exactly its shard (no work skipped or repeated), and no stream
+    # may have overflowed; a failed check ends every rank together (a lone exit would leave the others
+    # waiting in the next collective until the launcher's timeout)
+    shard_photons = 100 * (e - b) * args.steps
+    err = None
     if st["stream_overflow"]:
-        raise SystemExit(f"stream accumulation overflowed ({st['stream_overflow']} blocks dropped): lightmap invalid")
+        err = f"rank {rank}: stream accumulation overflowed ({st['stream_overflow']} blocks dropped): lightmap invalid"
+    elif int(st["photons"]) != shard_photons:
+        err = f"rank {rank}: photon counter {st['photons']} != its shard's {shard_photons}"
+    if world > 1:
+        bad = torch.tensor([1 if err else 0], dtype=torch.int32, device=dev)
+        parallel.all_reduce(bad, dist.ReduceOp.MAX)
+        if int(bad.item()) and not err:
+            err = f"rank {rank}: another rank failed its photon / overflow check"
+        if err:
+            dist.destroy_process_group()
+    if err:
+        raise SystemExit(err)
     span_ms = float(np.mean([s.elapsed_time(x) for s, x in k_ms]))  # whole fmgi_bake_items per step
     tim = ctx.timing()
     bake_launch_ms = tim["bake_ms"] / max(tim["bake_launches"], 1)  # the dominant kernel, per launch
     bake_launches = tim["bake_launches"]
-    # every rank's photon counter must cover exactly its shard (no work skipped or repeated)
-    shard_photons = 100 * (e - b) * args.steps
-    if int(st["photons"]) != shard_photons:
-        raise SystemExit(f"rank {rank}: photon counter {st['photons']} != its shard's {shard_photons}")
     if world > 1:  # per-rank breakdown, gathered to every rank (diagnoses the driver's multi-GPU runs)
         row = [float(rank), float(device_index), float(b), float(e), float(st["photons"]), bake_launch_ms,
                float(bake_launches) / args.steps, tim["fold_ms"] / args.steps, span_ms,
@@ -495,6 +514,7 @@ def main():
                 "texels": int(sc.num_texels),
                 "spa": spa,
                 "photons_per_step": photons_per_step,
+                "spa_clamped": spa_clamped,
                 "kernel": {0: "exact", 1: "fast", 2: "grid", 4: "hybrid"}[kernel if kernel != fmgi.KERNEL_AUTO else ctx.auto_kernel]
                 + (" (auto)" if kernel == fmgi.KERNEL_AUTO else ""),
                 "accumulation": {1: "fx3", 2: "state", 3: "none (PROFILING: deposits discarded)",

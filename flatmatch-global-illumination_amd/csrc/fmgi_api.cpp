@@ -259,19 +259,37 @@ struct GridBuild {
 };
 
 /* The quantized inline records of a grid cell (GridCell): the kernel's float ops, replayed in float32 on the
-   host (this file is built without FMA contraction). A record passes the float test iff
-   |fl(x - c)| <= hw; fl(x - c) is monotone in x, so the passing floats form an interval whose ends are
-   found by stepping one ulp at a time from c -/+ hw. */
+   host (this file is built without FMA contraction). A record passes the float test iff |fl(x - c)| <= hw;
+   fl(x - c) is monotone in x, so the passing floats form an interval [a, b] around c. Its ends are found
+   exactly by a binary search over the ordered float bit patterns between c and -/+infinity (64 steps at
+   most, whatever the ratio of hw to ulp(c)). */
 static bool grid_pass(float x, float c, float hw) {
     const float d = x - c;
     return fabsf(d) <= hw;
 }
-static float grid_end(float c, float hw, bool hi) {
-    float x = hi ? c + hw : c - hw;
-    const float out = hi ? INFINITY : -INFINITY, in = hi ? -INFINITY : INFINITY;
-    for (int k = 0; k < 64 && grid_pass(x, c, hw); k++) x = nextafterf(x, out); /* step out of the interval */
-    for (int k = 0; k < 128 && !grid_pass(x, c, hw); k++) x = nextafterf(x, in); /* back to its last float */
+/* a total order of the non-NaN floats as integers (-0 and +0 adjacent), and back */
+static int64_t float_key(float x) {
+    int32_t b;
+    memcpy(&b, &x, 4);
+    return b >= 0 ? (int64_t)b : -(int64_t)(b & 0x7FFFFFFF) - 1;
+}
+static float key_float(int64_t k) {
+    const int32_t b = k >= 0 ? (int32_t)k : (int32_t)((-(k + 1)) | 0x80000000ll);
+    float x;
+    memcpy(&x, &b, 4);
     return x;
+}
+/* the last float from c towards +/-infinity that passes the record test (c itself passes for hw >= 0) */
+static float grid_end(float c, float hw, bool hi) {
+    const int64_t kc = float_key(c), kinf = float_key(hi ? INFINITY : -INFINITY);
+    int64_t in = kc, out = kinf; /* in passes; out is the first key known to fail (or infinity) */
+    if (grid_pass(key_float(out), c, hw)) return key_float(out);
+    while (hi ? out - in > 1 : in - out > 1) {
+        const int64_t mid = in + (out - in) / 2;
+        if (grid_pass(key_float(mid), c, hw)) in = mid;
+        else out = mid;
+    }
+    return key_float(in);
 }
 /* q of float coordinate x in cell column `cell` of an axis with origin o and inverse cell size inv: the
    kernel's (x - o) * inv, minus the cell, times 2^16, clamped to [0, 65535] and truncated (grid_cell) */
@@ -283,8 +301,12 @@ static uint32_t grid_q(float x, float o, float inv, int cell) {
     return (uint32_t)std::min(std::max(m, 0.0f), 65535.0f);
 }
 static uint32_t grid_bounds(float c, float hw, float o, float inv, int cell) {
+    if (!(hw >= 0) || !grid_pass(c, c, hw)) return 0xFFFF0000u; /* (a degenerate record) pass-all */
     const float a = grid_end(c, hw, false), b = grid_end(c, hw, true);
-    if (!grid_pass(a, c, hw) || !grid_pass(b, c, hw)) return 0xFFFF0000u; /* (a degenerate record) pass-all */
+    /* the ends pass and the floats just outside them fail (the superset the kernel's bounds rely on) */
+    if (!grid_pass(a, c, hw) || !grid_pass(b, c, hw) || (a != -INFINITY && grid_pass(nextafterf(a, -INFINITY), c, hw)) ||
+        (b != INFINITY && grid_pass(nextafterf(b, INFINITY), c, hw)))
+        return 0xFFFF0000u;
     return grid_q(a, o, inv, cell) | (grid_q(b, o, inv, cell) << 16);
 }
 
@@ -713,6 +735,7 @@ struct fmgi_context {
     size_t blob_cap = 0;
     uint64_t blob_key = ~0ull;
     std::vector<RectLds> h_rects_lds; /* host staging of the LDS rect copy (kept until the copy is done) */
+    bool warned_cells = false;        /* the coarse LDS grid was launched unstaged (said once)          */
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -1413,7 +1436,9 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
        grid asks for it (kept only if the wave count holds); FMGI_CELLS_LDS=1 forces it for any grid or
        hybrid scan that fits, 0 turns it off (experiments) */
     const char *ce = getenv("FMGI_CELLS_LDS");
-    const bool cells_forced = ce && atoi(ce) == 1 && (kernel == FMGI_KERNEL_GRID || kernel == FMGI_KERNEL_HYBRID);
+    /* (only the grid scan reads the staged GridCell copy: ScanHybrid's grid walk reads GridCellF from global
+       memory, so staging for it would be dead LDS) */
+    const bool cells_forced = ce && atoi(ce) == 1 && kernel == FMGI_KERNEL_GRID;
     bool cells = cells_forced || (!ce && c->cells_lds && kernel == FMGI_KERNEL_GRID);
     auto best = [&](bool rects, int &bb, int &bw) {
         const int bytes = stage_bytes(c, kernel, rects, srcs, cells, nullptr, nullptr);
@@ -1568,6 +1593,13 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     }
     const StagePlan sp = plan_stage(c, kernel, kacc, trace);
     const int block = sp.block;
+    /* a closed box built with the coarse LDS grid (5 cells per record) but launched without the cells staged
+       reads that coarser grid from L2, slower than the 16-per-record grid it replaced: said once per context */
+    if (c->cells_lds && kernel == FMGI_KERNEL_GRID && sp.cells_off < 0 && !c->warned_cells && !getenv("FMGI_QUIET")) {
+        fprintf(stderr, "fmgi: the closed-box grid's cells (%d, built for LDS) are not staged at block %d: "
+                        "lookups read L2 (FMGI_CELLS_LDS=0 builds the finer global grid)\n", c->grid_cells, block);
+        c->warned_cells = true;
+    }
     if (c->nsrcs == 0) return set_err(FMGI_ERR_STATE, "no scene");
     /* no walls: every photon escapes at its first scan (photonmap.cl:208), so nothing is deposited */
     if (c->nrects == 0) return FMGI_OK;

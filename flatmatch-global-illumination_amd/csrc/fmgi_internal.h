@@ -214,7 +214,9 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
 constexpr int kAccBucket = 5;
 constexpr int kAccLines = 6; /* the bucket layout through per-workgroup tile lines (AccLines) */
 constexpr int kAccScatter = 7; /* the bucket layout stored lane by lane into per-wave tile blocks (AccScatter) */
+#ifndef FMGI_SCATTER_STRIDE
 #define FMGI_SCATTER_STRIDE 128 /* AccScatter: LDS dwords per wave (64 x {fill, block} words) */
+#endif
 constexpr int kAccDense = 8; /* a dense code stream (one code or sentinel per lane and iteration), binned by k_bin */
 /* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
    FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */

@@ -1686,6 +1686,10 @@ struct AccScatter {
                                                   uint32_t code) {
         u64 *T = tab(base);
         const uint32_t t = code >> (10 + FMGI_TILE_BITS);
+#if defined(FMGI_SCATTER_EXP) && FMGI_SCATTER_EXP == 2 /* PROFILING ONLY: no slot, no store; the codes xor-ed */
+        if (dep) T[64 + (threadIdx.x & 63)] ^= code; /* (a per-lane LDS word past the table: keeps the code live) */
+        return;
+#endif
         u64 old = 0;
         if (dep) old = __hip_atomic_fetch_add(T + t, 1ull, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         uint32_t rank = (uint32_t)old, blk = (uint32_t)(old >> 32);
@@ -1705,8 +1709,13 @@ struct AccScatter {
                 rank -= BP;
             }
         }
-#ifdef FMGI_SCATTER_EXP /* PROFILING ONLY: 1 = the slot is taken but the code is not stored (lightmap lost) */
+#ifdef FMGI_SCATTER_EXP /* PROFILING ONLY: 1 = the slot is taken but the code is not stored (lightmap lost);
+                           3 = stored coalesced to a fixed per-wave line instead of the slot */
         if (FMGI_SCATTER_EXP == 1 && code != 0xFFFFFFFEu) return;
+        if (FMGI_SCATTER_EXP == 3) {
+            if (dep) ((__attribute__((address_space(1))) uint32_t *)a.stream)[(uint64_t)(blockIdx.x * 16 + (threadIdx.x >> 6)) * 64 + (threadIdx.x & 63)] = code;
+            return;
+        }
 #endif
         if (dep) {
             if (blk != kNoBlock) ((__attribute__((address_space(1))) uint32_t *)a.stream)[(uint64_t)blk * BP + rank] = code;
@@ -1882,6 +1891,27 @@ __device__ __forceinline__ SrcDev load_src(const BakeArgs &a, const char *lds, i
     return src_fields(((gptr<SrcDev>)a.srcs)[srci]);
 }
 
+/* The sampler basis of a diffuse bounce (photonmap.cl:238 on the rect just hit): re-read from the rect table
+   at the top of the next iteration, from the workgroup's LDS copy when staged (BakeArgs::rects_off), instead of
+   being held in nine registers across the scan. FMGI_BASIS_RELOAD=0 builds keep the registers. */
+#ifndef FMGI_BASIS_RELOAD
+#define FMGI_BASIS_RELOAD 0
+#endif
+__device__ __forceinline__ void load_basis(const BakeArgs &a, const char *lds, int idx, f3 &n, f3 &bu, f3 &bv) {
+    if (uni(a.rects_off) >= 0) {
+        const __attribute__((address_space(3))) RectLds &r = *(const __attribute__((address_space(3))) RectLds *)(
+            (const __attribute__((address_space(3))) char *)lds + a.rects_off + __umul24((uint32_t)idx, (uint32_t)sizeof(RectLds)));
+        n = mkf3(r.nx, r.ny, r.nz);
+        bu = mkf3(r.bux, r.buy, r.buz);
+        bv = mkf3(r.bvx, r.bvy, r.bvz);
+    } else {
+        const gptr<RectDev> r = ((gptr<RectDev>)a.rects) + idx;
+        n = mkf3(r->nx, r->ny, r->nz);
+        bu = mkf3(r->bux, r->buy, r->buz);
+        bv = mkf3(r->bvx, r->bvy, r->bvz);
+    }
+}
+
 /* LCG^2: the two draws of a direction sample whose result is never used (last bounce) */
 __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
     constexpr uint32_t A2 = kJump.a[2], C2 = kJump.c[2];
@@ -1929,6 +1959,9 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
+#if FMGI_BASIS_RELOAD
+    int bidx = 0; /* the rect of the pending diffuse sample */
+#endif
     int depth = 0, left = 0, photon = -1, sid = 0, srci = 0;
     bool win = false, start = true, pend = false;
     uint64_t item = 0;
@@ -2009,6 +2042,9 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
             n_ph++;
         }
         sst.clk.lap(ST_START);
+#if FMGI_BASIS_RELOAD
+        if (!start && pend) load_basis(a, s_img, bidx, sn, sbu, sbv); /* the last hit's rect */
+#endif
         if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
         if (start) {
             const SrcDev S = load_src(a, s_img, srci);
@@ -2030,9 +2066,13 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         uint32_t code = 0;
         /* the basis of a diffuse sample at the top of the next iteration (unused unless pend is set; an
            escaped photon's next sample is an emission, whose basis the start block sets) */
+#if FMGI_BASIS_RELOAD
+        bidx = h.idx; /* (re-read there: one register held across the iteration instead of nine) */
+#else
         sn = mkf3(h.nx, h.ny, h.nz);
         sbu = mkf3(h.bux, h.buy, h.buz);
         sbv = mkf3(h.bvx, h.bvy, h.bvz);
+#endif
         if (h.best == INFINITY) { /* photonmap.cl:208-209 */
             start = true;
             n_esc++;

@@ -73,3 +73,21 @@ def test_radiosity_cpu_leg_runs():
     r = b.cpu_baseline_radiosity(procs=1)
     assert r["kind"] == "reference" and r["comparable"] is False and r["cores"] == 1
     assert r["unit"] == "form-factor rays/s" and r["value"] > 0
+
+
+def test_weak_scaling_spa_fits_the_reference_int_at_8_gpus():
+    """bench.py's weak configs run spa x N photons per area at N GPUs; numSamplesPerArea is an int in the
+    reference's interface (global_illumination_cl.h:10), so spa x 8 must stay <= INT_MAX for every config, and
+    a clamp (never hit by these configs) is reported instead of silently changing the workload."""
+    b = _bench()
+    for name, cfg in b.CONFIGS.items():
+        for n in (1, 2, 4, 8):
+            spa, clamped = b.weak_spa(cfg, n)
+            assert spa <= 2**31 - 1
+            if cfg["weak"]:
+                assert not clamped, (name, n)
+                assert spa == cfg["spa"] * n
+            else:
+                assert spa == cfg["spa"]
+    huge = {"spa": 2**30, "weak": True}
+    assert b.weak_spa(huge, 4) == (2**31 - 1, True)

@@ -67,6 +67,31 @@ def _entries(t, c):
     return np.concatenate([inline, t["recs"][rest]]), np.concatenate([ids, t["idx"][rest]]).astype(np.int32)
 
 
+def _fkey(x):
+    b = np.asarray(x, np.float32).view(np.int32).astype(np.int64)
+    return np.where(b >= 0, b, -(b & 0x7FFFFFFF) - 1)
+
+
+def _kfloat(k):
+    k = np.asarray(k, np.int64)
+    b = np.where(k >= 0, k, (-(k + 1)) | 0x80000000).astype(np.uint32)
+    return b.view(np.float32)
+
+
+def _interval_end(c, hw, hi):
+    """per record, the last float from c towards +/-inf with |fl(x - c)| <= hw (binary search on keys)"""
+    c, hw = np.asarray(c, np.float32), np.asarray(hw, np.float32)
+    inn = _fkey(c)
+    out = np.full_like(inn, int(_fkey(np.float32(np.inf if hi else -np.inf))))
+    for _ in range(70):
+        gap = np.abs(out - inn) > 1
+        mid = inn + (out - inn) // 2
+        ok = np.abs(_kfloat(mid) - c) <= hw
+        inn = np.where(gap & ok, mid, inn)
+        out = np.where(gap & ~ok, mid, out)
+    return _kfloat(inn)
+
+
 def _check_plane(t, p, cells, rng):
     per_cell = [_entries(t, c) for c in cells]
     recs = np.concatenate([r for r, _ in per_cell])
@@ -90,6 +115,16 @@ def _check_plane(t, p, cells, rng):
             v = np.nextafter(v, np.float32(np.inf) if sgn > 0 else np.float32(-np.inf)) if sgn else v
             us.append(cu)
             vs.append(v)
+    # the exact ends of each record's passing interval {x : |fl(x - c)| <= hw} (a binary search over the float
+    # bit patterns, independent of the host's), the floats one past them, and c -/+ hw -/+ ulp(c) / 2
+    for c, hw, other in ((cu, hwu, cv), (cv, hwv, cu)):
+        for hi in (False, True):
+            e = _interval_end(c, hw, hi)
+            past = np.nextafter(e, np.float32(np.inf) if hi else np.float32(-np.inf))
+            half = (c + (hw if hi else -hw) + (1 if hi else -1) * np.spacing(c) / 2).astype(np.float32)
+            for x in (e, past, half):
+                us.append(x if c is cu else other)
+                vs.append(other if c is cu else x)
     lo_u, hi_u = float((cu - hwu).min()), float((cu + hwu).max())
     lo_v, hi_v = float((cv - hwv).min()), float((cv + hwv).max())
     us.append(rng.uniform(lo_u, hi_u, 20000).astype(np.float32))
