@@ -1163,9 +1163,7 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
            vs 3.65e9 photons/s FAST, 3.02e9 GRID) when the floor/ceiling records share few planes */
         if (c->auto_kernel == FMGI_KERNEL_FAST && 4 * gb.J[2] < fb.J[2]) c->auto_kernel = FMGI_KERNEL_HYBRID;
         /* the largest LDS use (STREAM rings) decides, so the choice holds for every accumulation mode */
-        const char *se = getenv("FMGI_SCATTER");
-        c->auto_kernel = fitting_kernel(c, c->auto_kernel, (se && atoi(se) == 1) ? kAccScatter : FMGI_ACCUM_STREAM,
-                                        bake_block());
+        c->auto_kernel = fitting_kernel(c, c->auto_kernel, FMGI_ACCUM_STREAM, bake_block());
     }
     if (c->device != FMGI_HOST_ONLY) {
     HIPCHK(hipSetDevice(c->device));
@@ -1562,8 +1560,15 @@ static int exec_accum(const fmgi_context *c) {
     if (c->accum != FMGI_ACCUM_STREAM || stream_layout(c) != kStreamBuckets) return c->accum;
     const char *le = getenv("FMGI_LINES");
     if (le && atoi(le) == 1) return kAccLines;
+    /* AUTO: the lane-by-lane stores (AccScatter) when the scene's wall table (and the closed box's grid cells)
+       fit in LDS beside the image, so the bake loop reads no global memory and the scattered stores' slow
+       completions never hold up a load's s_waitcnt (box200: bake 76.7 -> 69.3 ms at 6 instead of 4 waves per
+       SIMD; box2000, whose 2000 walls stay in L2: 132 ms with the rings, 160 with scattered stores; profiles/
+       r05/s5). FMGI_SCATTER=0/1 forces either (experiments, tests). */
     const char *se = getenv("FMGI_SCATTER");
-    return (se && atoi(se) == 1) ? kAccScatter : kAccBucket;
+    if (se) return atoi(se) == 1 ? kAccScatter : kAccBucket;
+    const size_t tables = (size_t)c->nrects * sizeof(RectLds) + (c->cells_lds ? (size_t)c->grid_cells * sizeof(GridCell) : 0);
+    return tables <= 64 * 1024 ? kAccScatter : kAccBucket;
 }
 
 static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int kernel, hipStream_t s, bool trace,
