@@ -1368,8 +1368,8 @@ struct StagePlan {
     int rects_off = -1, srcs_off = -1, cells_off = -1, grecs_off = -1, gidx_off = -1;
 };
 
-static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, bool cells, int *roff, int *soff,
-                       int *coff = nullptr, int *groff = nullptr, int *gioff = nullptr) {
+static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, bool cells, bool grecs, int *roff,
+                       int *soff, int *coff = nullptr, int *groff = nullptr, int *gioff = nullptr) {
     int off = (image_bytes(c, kernel) + 15) & ~15;
     if (roff) *roff = rects ? off : -1;
     if (rects) off += c->nrects * (int)sizeof(RectLds);
@@ -1378,11 +1378,12 @@ static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs,
     off = (off + 15) & ~15;
     if (coff) *coff = cells ? off : -1;
     if (cells) off += c->grid_cells * (int)sizeof(GridCell);
-    /* with the cells (FMGI_GRECS_LDS=1, experiments), the overflow records of cells of more than two
-       (float4) and their rect indices: box200 bake 76.65 -> 77.16 ms (profiles/r04/s26), so by default
-       they stay in global memory */
+    /* with the cells, the overflow records of cells of more than two (float4) and their rect indices
+       (`grecs`): the lane-by-lane stores' instance stages them (then its bake loop reads no global memory at
+       all, FMGI_KVAR_STAGED); the rings' instance keeps them in global memory (box200 bake 76.65 -> 77.16 ms
+       with them staged at 4 waves/SIMD, profiles/r04/s26). FMGI_GRECS_LDS=0/1 forces (experiments). */
     const char *ge = getenv("FMGI_GRECS_LDS");
-    const bool ov = cells && ge && atoi(ge) == 1;
+    const bool ov = cells && (ge ? atoi(ge) == 1 : grecs);
     if (groff) *groff = ov ? off : -1;
     if (ov) off += c->grid_entries * 16;
     if (gioff) *gioff = ov ? off : -1;
@@ -1439,7 +1440,7 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     const bool cells_forced = ce && atoi(ce) == 1 && kernel == FMGI_KERNEL_GRID;
     bool cells = cells_forced || (!ce && c->cells_lds && kernel == FMGI_KERNEL_GRID);
     auto best = [&](bool rects, int &bb, int &bw) {
-        const int bytes = stage_bytes(c, kernel, rects, srcs, cells, nullptr, nullptr);
+        const int bytes = stage_bytes(c, kernel, rects, srcs, cells, accum == kAccScatter, nullptr, nullptr);
         bb = p.block;
         bw = waves(p.block, bytes);
         if (forced_block) return;
@@ -1473,16 +1474,18 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
         }
     }
     p.block = rects ? b1 : b0;
-    p.bytes = stage_bytes(c, kernel, rects, srcs, cells, &p.rects_off, &p.srcs_off, &p.cells_off, &p.grecs_off,
+    p.bytes = stage_bytes(c, kernel, rects, srcs, cells, accum == kAccScatter, &p.rects_off, &p.srcs_off, &p.cells_off,
+                          &p.grecs_off,
                           &p.gidx_off);
     return p;
 }
 
-static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, int lds, uint64_t items) {
+static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace, int block, int lds, uint64_t items,
+                       int inst = -1) {
     /* persistent grid: exactly the blocks that are resident at once (occupancy from the VGPR/SGPR/LDS
        use of the kernel actually launched), so no block starts late and lengthens the tail; never more
        lanes than work items */
-    int per_cu = fmgi_bake_resident_blocks(kernel_instance(c, kernel), accum, trace, block, lds);
+    int per_cu = fmgi_bake_resident_blocks(inst >= 0 ? inst : kernel_instance(c, kernel), accum, trace, block, lds);
     if (per_cu <= 0) per_cu = 4;
     if (const char *pe = getenv("FMGI_BAKE_WG_PER_CU")) /* experiments: leave room for concurrent folds */
         if (atoi(pe) > 0) per_cu = std::min(per_cu, atoi(pe));
@@ -1557,6 +1560,7 @@ static int stream_layout(const fmgi_context *c) {
    (kAccBucket) or through per-workgroup tile lines (kAccLines, FMGI_LINES=1) */
 static int exec_accum(const fmgi_context *c) {
     if (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamDense) return kAccDense;
+    if (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamSliced) return kAccSliced;
     if (c->accum != FMGI_ACCUM_STREAM || stream_layout(c) != kStreamBuckets) return c->accum;
     const char *le = getenv("FMGI_LINES");
     if (le && atoi(le) == 1) return kAccLines;
@@ -1598,6 +1602,13 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     }
     const StagePlan sp = plan_stage(c, kernel, kacc, trace);
     const int block = sp.block;
+    /* the closed box with every table staged (walls, emitters, grid cells) launches the instance whose
+       global-memory paths for them are compiled out (FMGI_KVAR_STAGED); FMGI_NO_STAGED=1 (experiments) keeps
+       the general one */
+    int inst = kernel_instance(c, kernel);
+    if (inst == (FMGI_KERNEL_GRID | FMGI_KVAR_AXES) && sp.rects_off >= 0 && sp.srcs_off >= 0 && sp.cells_off >= 0 &&
+        sp.grecs_off >= 0 && !getenv("FMGI_NO_STAGED"))
+        inst |= FMGI_KVAR_STAGED;
     /* a closed box built with the coarse LDS grid (5 cells per record) but launched without the cells staged
        reads that coarser grid from L2, slower than the 16-per-record grid it replaced: said once per context */
     if (c->cells_lds && kernel == FMGI_KERNEL_GRID && sp.cells_off < 0 && !c->warned_cells && !getenv("FMGI_QUIET")) {
@@ -1851,8 +1862,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), kacc, trace,
-                                grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop),
+        HIPCHK(fmgi_launch_bake(a, a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace,
+                                grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop,
+                                            a.coop > 1 ? -1 : inst),
                                 block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         /* AccState: fold the (state, texel) counters into the int64 lightmap and zero them */
@@ -1892,7 +1904,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
         const int k = overlap ? (nchunk & 1) : 0; /* one buffer set unless the folds run beside the bakes */
-        const int grid = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (ce - cb) * (uint64_t)a.coop);
+        const int grid = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (ce - cb) * (uint64_t)a.coop,
+                                     a.coop > 1 ? -1 : inst);
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));
@@ -1929,10 +1942,10 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         hipEvent_t t0 = nullptr, t1 = nullptr;
         if (getenv("FMGI_SHOW_LAUNCH")) /* experiments: the launch shape the planner chose */
             fprintf(stderr, "fmgi: bake kernel %d accum %d block %d grid %d lds %zu (staged %d: rects %d srcs %d cells %d)\n",
-                    kernel_instance(c, kernel), kacc, block, grid, fmgi_bake_lds(kernel_instance(c, kernel), kacc, block, a.fimg_bytes, nullptr),
+                    a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, block, grid, fmgi_bake_lds(kernel_instance(c, kernel), kacc, block, a.fimg_bytes, nullptr),
                     a.fimg_bytes, a.rects_off, a.srcs_off, a.cells_off);
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, kernel_instance(c, kernel), kacc, trace, grid, block, s));
+        HIPCHK(fmgi_launch_bake(a, a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace, grid, block, s));
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         if (overlap) {
             HIPCHK(hipEventRecord(c->ev_baked[k], s));

@@ -218,10 +218,12 @@ constexpr int kAccScatter = 7; /* the bucket layout stored lane by lane into per
 #define FMGI_SCATTER_STRIDE 128 /* AccScatter: LDS dwords per wave (64 x {fill, block} words) */
 #endif
 constexpr int kAccDense = 8; /* a dense code stream (one code or sentinel per lane and iteration), binned by k_bin */
+constexpr int kAccSliced = 9; /* the STREAM's unsorted layout alone (BakeArgs::presort 0, AccStreamT<0>) */
 /* `kernel` of the bake launch helpers below: the public FMGI_KERNEL_* id, or FMGI_KERNEL_GRID |
    FMGI_KVAR_AXES for the closed-box instance of the grid scan (BakeArgs::grid_axes set) */
 #define FMGI_KVAR_AXES 0x100
 #define FMGI_KVAR_PLAN 0x200 /* FMGI_KERNEL_HYBRID | this: the walls over the floor plan (BakeArgs::plan_off) */
+#define FMGI_KVAR_STAGED 0x400 /* FMGI_KERNEL_GRID | FMGI_KVAR_AXES | this: walls, emitters and cells all in LDS */
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);

@@ -126,8 +126,9 @@ __device__ __forceinline__ float exact_hit_rec(const R &r, int idx, f3 src, f3 d
 /* the same on rect idx, read from the workgroup's LDS copy of the table (RectLds records) when the host
    staged it there (BakeArgs::rects_off >= 0), else from global memory; the two reads stay in their own address
    spaces (a pointer that may be either compiles to flat loads, which wait on both counters) */
+template <bool Staged = false>
 __device__ __forceinline__ float exact_hit(const BakeArgs &a, const char *lds, int idx, f3 src, f3 dir, HitRec &h) {
-    if (uni(a.rects_off) >= 0)
+    if (Staged || uni(a.rects_off) >= 0)
         return exact_hit_rec(*(const __attribute__((address_space(3))) RectLds *)(
                                  (const __attribute__((address_space(3))) char *)lds + a.rects_off +
                                  __umul24((uint32_t)idx, (uint32_t)sizeof(RectLds))), /* not the quarter-rate v_mul_lo_u32 */
@@ -147,6 +148,11 @@ __device__ __forceinline__ void finish_hit(const BakeArgs &a, int hit, float bes
     if (hit >= 0 && best != INFINITY)
         exact_hit(a, hit, src, dir, h); /* the same fac again: closest never changes intersects()' fac */
     h.best = best;
+    /* (rare path) the record's fields are in registers before the bake loop goes on: none of the
+       loop-carried registers (the sample basis) is left pending on a global load, which would make the
+       compiler wait vmcnt(0) at the loop's top, i.e. for the scattered deposit store of the iteration before
+       (gfx9 counts stores in vmcnt) */
+    __builtin_amdgcn_s_waitcnt(0x0F70); /* vmcnt(0) */
 }
 
 /* ---- scan policies -------------------------------------------------------------------------- */
@@ -419,10 +425,11 @@ __device__ __forceinline__ uint32_t grid_cell(const float4 g0, const float4 g1, 
    (BakeArgs::cells_off >= 0), else from global memory (L2-resident). The two reads stay in their own
    address spaces: a pointer that may point into either compiles to flat loads, which count in both
    vmcnt and lgkmcnt and make every LDS wait after them wait for the cell too. */
+template <bool Staged = false>
 __device__ __forceinline__ GridCell load_cell(const BakeArgs &a, const char *lds, uint32_t ci) {
     typedef uint32_t u4 __attribute__((ext_vector_type(4)));
     u4 q, r;
-    if (uni(a.cells_off) >= 0) {
+    if (Staged || uni(a.cells_off) >= 0) {
         const __attribute__((address_space(3))) u4 *l = (const __attribute__((address_space(3))) u4 *)(
             (const __attribute__((address_space(3))) char *)lds + a.cells_off);
         q = l[2 * ci];
@@ -463,6 +470,7 @@ __device__ __forceinline__ void grid_recq(float f, uint32_t qu, uint32_t qv, uin
 
 /* the candidate tests of one cell: its two inline records (quantized bounds; absent ones are never
    candidates), then its overflow records (float, rare); code1 receives the winner's rect index */
+template <bool Staged = false>
 __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const char *lds, const GridCell &c, float f,
                                                 float uh, float vh, uint32_t qu, uint32_t qv, float &L1, float &L2,
                                                 int &code1, unsigned &ntest) {
@@ -470,7 +478,7 @@ __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const char *l
     grid_recq(f, qu, qv, c.qu0, c.qv0, c.idx0 | a.grid_code_or, L1, L2, code1);
     grid_recq(f, qu, qv, c.qu1, c.qv1, c.idx1 | a.grid_code_or, L1, L2, code1);
     if (c.count > 2) {
-        if (uni(a.grecs_off) >= 0) { /* the overflow records staged beside the cells */
+        if (Staged || uni(a.grecs_off) >= 0) { /* the overflow records staged beside the cells */
             typedef float f4v __attribute__((ext_vector_type(4)));
             const __attribute__((address_space(3))) char *l = (const __attribute__((address_space(3))) char *)lds;
             const __attribute__((address_space(3))) f4v *recs =
@@ -669,7 +677,7 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
  * winner's exact fac f, so the separation test `L2 > f (1 + 2^-12)` has the same outcome with or
  * without it (grid_phase1_sorted's argument); equal keys fail that test whatever the order.
  */
-template <int A>
+template <int A, bool Staged>
 __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *img, f3 s, f3 d, float f, float &L1,
                                                 float &L2, int &code1, unsigned &ntest) {
     constexpr int U = (A == 0) ? 1 : 0;
@@ -678,9 +686,10 @@ __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *i
     const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
     uint32_t qu, qv;
     const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-    grid_cell_tests(a, img, load_cell(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
+    grid_cell_tests<Staged>(a, img, load_cell<Staged>(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
 }
 
+template <bool Staged>
 __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
                                                  float &L2, int &code1, unsigned &ntest) {
     const float fx0 = (*(const float *)(img + (d.x < 0.0f ? 0 : 64)) - s.x) * __builtin_amdgcn_rcpf(d.x);
@@ -703,16 +712,16 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
         const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
         uint32_t qu, qv;
         const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-        grid_cell_tests(a, img, load_cell(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
+        grid_cell_tests<Staged>(a, img, load_cell<Staged>(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
     }
     const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
-    if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0>(a, img, s, d, fx, L1, L2, code1, ntest);
-    if (m != 1 && fy < INFINITY && fy <= L1 * 1.00048828125f) grid_axes_visit<1>(a, img, s, d, fy, L1, L2, code1, ntest);
-    if (m != 2 && fz < INFINITY && fz <= L1 * 1.00048828125f) grid_axes_visit<2>(a, img, s, d, fz, L1, L2, code1, ntest);
+    if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0, Staged>(a, img, s, d, fx, L1, L2, code1, ntest);
+    if (m != 1 && fy < INFINITY && fy <= L1 * 1.00048828125f) grid_axes_visit<1, Staged>(a, img, s, d, fy, L1, L2, code1, ntest);
+    if (m != 2 && fz < INFINITY && fz <= L1 * 1.00048828125f) grid_axes_visit<2, Staged>(a, img, s, d, fz, L1, L2, code1, ntest);
 }
 
 /* calls fn(idx) for the rect index of every record that passes grid_axis's candidate test */
-template <int A, class F>
+template <int A, bool FloatCells, class F>
 __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, int off, int J, f3 s, f3 d, F &&fn) {
     const char *img = lds + off;
     constexpr int U = (A == 0) ? 1 : 0;
@@ -727,13 +736,24 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
         const float f = (g0.x - sa) * rd;
         if (!(f >= 0.0f)) continue;
         const float uh = fmaf(du, f, su), vh = fmaf(dv, f, sv);
-        uint32_t qu, qv;
-        const GridCell c = load_cell(a, lds, grid_cell(g0, g1, g2, uh, vh, qu, qv));
-        if (c.count > 0 && grid_qpass(qu, qv, c.qu0, c.qv0)) fn(c.idx0);
-        if (c.count > 1 && grid_qpass(qu, qv, c.qu1, c.qv1)) fn(c.idx1);
-        for (int k = 2; k < c.count; k++) {
-            const float4 r = recs[c.rest + k - 2];
-            if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[c.rest + k - 2]);
+        int count, rest;
+        if (FloatCells) { /* the general walks' cells (GridCellF): the same float tests as their phase 1 */
+            typedef float f4v __attribute__((ext_vector_type(4)));
+            const gptr<f4v> cp = (gptr<f4v>)a.gcellsF + 3 * grid_cell_idx(g0, g1, g2, uh, vh);
+            const f4v r0 = cp[0], r1 = cp[1], r2 = cp[2];
+            count = __float_as_int(r2.x), rest = __float_as_int(r2.w);
+            if (count > 0 && (int)(fabsf(uh - r0.x) <= r0.y) & (int)(fabsf(vh - r0.z) <= r0.w)) fn(__float_as_int(r2.y));
+            if (count > 1 && (int)(fabsf(uh - r1.x) <= r1.y) & (int)(fabsf(vh - r1.z) <= r1.w)) fn(__float_as_int(r2.z));
+        } else {
+            uint32_t qu, qv;
+            const GridCell c = load_cell(a, lds, grid_cell(g0, g1, g2, uh, vh, qu, qv));
+            count = c.count, rest = c.rest;
+            if (c.count > 0 && grid_qpass(qu, qv, c.qu0, c.qv0)) fn(c.idx0);
+            if (c.count > 1 && grid_qpass(qu, qv, c.qu1, c.qv1)) fn(c.idx1);
+        }
+        for (int k = 2; k < count; k++) {
+            const float4 r = recs[rest + k - 2];
+            if ((int)(fabsf(uh - r.x) <= r.y) & (int)(fabsf(vh - r.z) <= r.w)) fn(a.gridx[rest + k - 2]);
         }
     }
 }
@@ -741,10 +761,14 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
 /* Axes = true: the closed-box specialisation (one plane per axis and class, BakeArgs::grid_axes), whose
    kernel holds grid_phase1_axes alone: the general kernel's register and SGPR budget is set by its layout
    walks, and its spilled SGPRs come back as v_readlane in the box scan too */
-template <bool Axes>
+template <bool Axes, bool Staged = false>
 struct ScanGridT {
     static constexpr bool kLds = true;
     static constexpr bool kCoop = false;
+    /* Staged (closed boxes whose walls, emitters, grid cells and the cells' overflow records the plan stages
+       in LDS): the global-memory paths of those tables are compiled out, so the bake loop issues no global
+       load but its rare fallbacks' and work-item fetches' */
+    static constexpr bool kStaged = Staged;
     static constexpr int kMinWaves = 4; /* k_bake occupancy floor for the register allocator */
     static constexpr int kOrderedRounds = 12;
 
@@ -763,9 +787,9 @@ struct ScanGridT {
             /* the closed-box instance knows its plane counts ({1, 1, 1}): constants, not uniform masks
                the register allocator would keep live across the bake loop */
             const int J0 = Axes ? 1 : a.fJ[0], J1 = Axes ? 1 : a.fJ[1], J2 = Axes ? 1 : a.fJ[2];
-            grid_visit<0>(a, lds, 0, J0, src, dir, take);
-            grid_visit<1>(a, lds, 128 * J0, J1, src, dir, take);
-            grid_visit<2>(a, lds, 128 * (J0 + J1), J2, src, dir, take);
+            grid_visit<0, true>(a, lds, 0, J0, src, dir, take);
+            grid_visit<1, true>(a, lds, 128 * J0, J1, src, dir, take);
+            grid_visit<2, true>(a, lds, 128 * (J0 + J1), J2, src, dir, take);
             for (int g = 0; g < uni(a.ngeneral); g++) {
                 const int idx = a.general[g];
                 if (idx > prev && idx < nxt && exact_on_v(a.rects, idx, src, dir, INFINITY) >= 0) nxt = idx;
@@ -790,7 +814,7 @@ struct ScanGridT {
         int code1 = -1;
         unsigned ntest = 0;
         if (Axes) {
-            grid_phase1_axes(a, lds, src, dir, L1, L2, code1, ntest);
+            grid_phase1_axes<Staged>(a, lds, src, dir, L1, L2, code1, ntest);
         } else if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
             grid_phase1_sorted(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
@@ -822,7 +846,7 @@ struct ScanGridT {
             return;
         }
         const int idx = code1; /* rect index of the phase-1 winner */
-        const float f = exact_hit(a, lds, idx, src, dir, h);
+        const float f = exact_hit<Staged>(a, lds, idx, src, dir, h);
         const bool sep = !(f < 0) && L2 > f * 1.000244140625f; /* ScanFast's separation test */
         st.clk.lap(ST_SCAN2);
         if (sep) {
@@ -840,6 +864,7 @@ struct ScanGridT {
 
 using ScanGrid = ScanGridT<false>;
 using ScanGridAxes = ScanGridT<true>;
+using ScanGridAxesStaged = ScanGridT<true, true>;
 
 /*
  * ScanHybrid's wall pass over the floor plan (Plan = true; tables: fmgi_api.cpp build_plan, which holds
@@ -1459,6 +1484,9 @@ struct AccStreamT {
 };
 
 using AccStream = AccStreamT<-1>; /* unsorted codes / presorted segments (BakeArgs::presort 0, 1) */
+using AccSliced = AccStreamT<0>;  /* unsorted codes only (lightmaps of more than 63 tiles): the instance
+                                     holds none of the presort / bucket code, whose registers and SGPR
+                                     spills made the 30-room layout's bake 16 % slower (profiles/r05/s10) */
 using AccBucket = AccStreamT<2>;  /* per-tile buckets (BakeArgs::presort 2) */
 
 /*
@@ -1717,8 +1745,21 @@ struct AccScatter {
             return;
         }
 #endif
+        /* Drain the vector-memory counter BEFORE the store (normally only the previous iteration's store is
+           still counted, long since written). Loop-carried registers that some rare path fills with global
+           loads (the rect and emitter tables' global fallbacks) otherwise make the compiler wait vmcnt(0) at
+           the top of the next iteration, and gfx9 counts stores in vmcnt in issue order: every iteration
+           would wait for this store's completion (profiles/r05/s8). */
+#ifndef FMGI_SCATTER_DRAIN
+#define FMGI_SCATTER_DRAIN 0
+#endif
+        if (FMGI_SCATTER_DRAIN) __builtin_amdgcn_s_waitcnt(0x0F70); /* vmcnt(0), expcnt / lgkmcnt untouched */
         if (dep) {
+#ifdef FMGI_SCATTER_NT /* experiments: non-temporal stores */
+            if (blk != kNoBlock) __builtin_nontemporal_store(code, ((__attribute__((address_space(1))) uint32_t *)a.stream) + ((uint64_t)blk * BP + rank));
+#else
             if (blk != kNoBlock) ((__attribute__((address_space(1))) uint32_t *)a.stream)[(uint64_t)blk * BP + rank] = code;
+#endif
             else AccBucket::bucket_atomic(a, code);
         }
     }
@@ -1883,9 +1924,20 @@ __device__ __forceinline__ SrcDev src_fields(const R &r) {
     return d;
 }
 
+/* whether a scan's instance compiles the tables' global paths out (ScanGridT::kStaged) */
+template <class Scan, class = void>
+struct ScanStaged {
+    static constexpr bool value = false;
+};
+template <class Scan>
+struct ScanStaged<Scan, decltype((void)Scan::kStaged)> {
+    static constexpr bool value = Scan::kStaged;
+};
+
 /* emitter srci: from the workgroup's LDS copy of the SrcDev table when staged (BakeArgs::srcs_off >= 0) */
+template <bool Staged = false>
 __device__ __forceinline__ SrcDev load_src(const BakeArgs &a, const char *lds, int srci) {
-    if (uni(a.srcs_off) >= 0)
+    if (Staged || uni(a.srcs_off) >= 0)
         return src_fields(((const __attribute__((address_space(3))) SrcDev *)(
             (const __attribute__((address_space(3))) char *)lds + a.srcs_off))[srci]);
     return src_fields(((gptr<SrcDev>)a.srcs)[srci]);
@@ -2028,7 +2080,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                 photon = -1;
                 nev = 0;
             }
-            const SrcDev S = load_src(a, s_img, srci);
+            const SrcDev S = load_src<ScanStaged<Scan>::value>(a, s_img, srci);
             col = win ? mkf3(18, 18, 18) : mkf3(16, 16, 18); /* photonmap.cl:167-169 */
             sid = win ? (512 + 1) : 1; /* colour state: source kind, then one bit per diffuse bounce */
             edx = rng_next(rng);
@@ -2047,7 +2099,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
 #endif
         if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
         if (start) {
-            const SrcDev S = load_src(a, s_img, srci);
+            const SrcDev S = load_src<ScanStaged<Scan>::value>(a, s_img, srci);
             pos = add3(add3(add3(mkf3(S.px, S.py, S.pz), mul3(mkf3(S.wx, S.wy, S.wz), edx)),
                             mul3(mkf3(S.hx, S.hy, S.hz), edy)),
                        mul3(dir, 1e-5f));
@@ -2329,6 +2381,7 @@ const void *kernel_acc(int accum, bool trace) {
     if (accum == 2) return kernel_ptr<Scan, AccState>(trace);
     if (accum == 3) return kernel_ptr<Scan, AccNone>(trace);
     if (accum == 4) return kernel_ptr<Scan, AccStream>(trace);
+    if (accum == kAccSliced) return kernel_ptr<Scan, AccSliced>(trace);
     if (accum == kAccBucket) return kernel_ptr<Scan, AccBucket>(trace);
     if (accum == kAccLines) return kernel_ptr<Scan, AccLines>(trace);
     if (accum == kAccScatter) return kernel_ptr<Scan, AccScatter>(trace);
@@ -2341,6 +2394,7 @@ void launch_acc(const BakeArgs &a, int accum, bool trace, dim3 grid, dim3 block,
     if (accum == 2) launch3<Scan, AccState>(a, trace, grid, block, lds, s);
     else if (accum == 3) launch3<Scan, AccNone>(a, trace, grid, block, lds, s);
     else if (accum == 4) launch3<Scan, AccStream>(a, trace, grid, block, lds, s);
+    else if (accum == kAccSliced) launch3<Scan, AccSliced>(a, trace, grid, block, lds, s);
     else if (accum == kAccBucket) launch3<Scan, AccBucket>(a, trace, grid, block, lds, s);
     else if (accum == kAccLines) launch3<Scan, AccLines>(a, trace, grid, block, lds, s);
     else if (accum == kAccScatter) launch3<Scan, AccScatter>(a, trace, grid, block, lds, s);
@@ -2354,10 +2408,12 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
                : accum == kAccLines ? kernel_ptr<ScanFastCoop, AccLines>(false)
                : accum == kAccScatter ? kernel_ptr<ScanFastCoop, AccScatter>(false)
                : accum == kAccDense ? kernel_ptr<ScanFastCoop, AccDense>(false)
+               : accum == kAccSliced ? kernel_ptr<ScanFastCoop, AccSliced>(false)
                                     : kernel_ptr<ScanFastCoop, AccStream>(false);
+    if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) return kernel_acc<ScanGridAxesStaged>(accum, trace);
     if (kernel == (2 | FMGI_KVAR_AXES)) return kernel_acc<ScanGridAxes>(accum, trace);
     if (kernel == (4 | FMGI_KVAR_PLAN)) return kernel_acc<ScanHybridPlan>(accum, trace);
-    kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN);
+    kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN | FMGI_KVAR_STAGED);
     if (kernel == 2) return kernel_acc<ScanGrid>(accum, trace);
     if (kernel == 4) return kernel_acc<ScanHybrid>(accum, trace);
     if (kernel == 1) return kernel_acc<ScanFast>(accum, trace);
@@ -2376,7 +2432,7 @@ size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_
     if (accum == kAccLines) return img + (size_t)FMGI_LINES_DWORDS * 4;
     if (accum == kAccScatter) return img + (size_t)(block / 64) * FMGI_SCATTER_STRIDE * 4;
     if (accum == kAccBucket) return img + (size_t)(block / 64) * FMGI_RING_STRIDE_BUCKET * 4;
-    return img + (accum == 4 ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
+    return img + ((accum == 4 || accum == kAccSliced) ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
 }
 
 /* a bake launch of more than 64 KiB of dynamic LDS (scan image + staged tables + rings, fmgi_api.cpp
@@ -2416,18 +2472,22 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         if (e != hipSuccess) return e;
     }
     if (kernel == FMGI_KERNEL_FAST_COOP) {
-        if ((accum != 4 && accum != kAccBucket && accum != kAccLines && accum != kAccScatter && accum != kAccDense) ||
+        if ((accum != 4 && accum != kAccBucket && accum != kAccLines && accum != kAccScatter && accum != kAccDense &&
+             accum != kAccSliced) ||
             trace)
             return hipErrorInvalidValue;
         if (accum == kAccBucket) launch3<ScanFastCoop, AccBucket>(a, false, grid, blk, lds, s);
         else if (accum == kAccScatter) launch3<ScanFastCoop, AccScatter>(a, false, grid, blk, lds, s);
         else if (accum == kAccDense) launch3<ScanFastCoop, AccDense>(a, false, grid, blk, lds, s);
+        else if (accum == kAccSliced) launch3<ScanFastCoop, AccSliced>(a, false, grid, blk, lds, s);
         else if (accum == kAccLines) launch3<ScanFastCoop, AccLines>(a, false, grid, blk, lds, s);
         else launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
     } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */
         launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
         launch_acc<ScanHybrid>(a, accum, trace, grid, blk, lds, s);
+    } else if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) { /* closed box, every table in LDS */
+        launch_acc<ScanGridAxesStaged>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES)) { /* FMGI_KERNEL_GRID, closed box */
         launch_acc<ScanGridAxes>(a, accum, trace, grid, blk, lds, s);
     } else if ((kernel & ~FMGI_KVAR_AXES) == 2) { /* FMGI_KERNEL_GRID */
