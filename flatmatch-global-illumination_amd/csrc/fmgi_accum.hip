@@ -328,7 +328,7 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
    was slower. */
 /* 8 waves per SIMD (<= 64 VGPRs): two 1024-lane workgroups per CU, as their 64 KB of LDS allow (at 66
    VGPRs only one fitted, and the fold took 13.7 ms instead of 11) */
-template <int EXP>
+template <int EXP, int TB = FMGI_TILE_BITS>
 __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restrict__ pool,
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ block_len,
@@ -336,6 +336,7 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
                                                      int balanced, const uint4 *__restrict__ colpack,
                                                      unsigned long long *__restrict__ lm, int num_texels) {
     constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
+    constexpr int kTileTexels = 1 << TB; /* this instance's fold tile */
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
     unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
@@ -483,7 +484,8 @@ __global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restri
                                                      int P, uint32_t *__restrict__ pool,
                                                      uint32_t *__restrict__ block_tile, uint32_t *__restrict__ block_len,
                                                      unsigned long long *__restrict__ pool_cursor, uint64_t pool_blocks,
-                                                     const uint4 *__restrict__ colpack, unsigned long long *__restrict__ lm) {
+                                                     const uint4 *__restrict__ colpack, unsigned long long *__restrict__ lm,
+                                                     uint32_t shift) {
     constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
     extern __shared__ __attribute__((aligned(16))) uint32_t stage[]; /* kBinBatch codes */
     __shared__ uint32_t hist[16][64];
@@ -495,7 +497,6 @@ __global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restri
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
     const uint64_t nbatch = (n + kBinBatch - 1) / kBinBatch;
     if (threadIdx.x < 64) info[threadIdx.x] = make_uint2(kNoBlk, BP);
-    const uint32_t shift = 10 + FMGI_TILE_BITS;
     typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
     for (uint64_t b = blockIdx.x; b < nbatch; b += gridDim.x) {
         /* the wave's kBinPer * 64 codes (n is a multiple of FMGI_STREAM_BLOCK: a wave's part is all in or out) */
@@ -582,7 +583,7 @@ __global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restri
                 }
                 tab[lane] = make_uint4(tstart[lane], first, inf.x, b0);
                 tfill[lane] = inf.y;
-                if (nnew) info[lane] = make_uint2(b0, b0 == kNoBlk ? 0u : rest - (nnew - 1) * BP);
+                if (nnew) info[lane] = b0 == kNoBlk ? make_uint2(kNoBlk, 0u) : make_uint2(b0 + nnew - 1, rest - (nnew - 1) * BP);
                 else info[lane] = make_uint2(inf.x, inf.y + x);
             }
         }
@@ -613,14 +614,16 @@ __global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restri
 } // namespace
 
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s) {
-    const int P = (num_texels + kTileTexels - 1) / kTileTexels;
-    const size_t plds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16;
+    /* the bucket layouts' tiles may be wide (sb.tile_bits); the others are FMGI_TILE_BITS */
+    const int tb = sb.presort >= 2 && sb.tile_bits > 0 ? sb.tile_bits : FMGI_TILE_BITS;
+    const int P = (num_texels + (1 << tb) - 1) >> tb;
+    const size_t plds = (size_t)3 * ((size_t)1 << tb) * 8 + (size_t)FMGI_COLOUR_STATES * 16;
     if (sb.presort == 3) { /* the dense stream: binned into the pool, then folded as the bucket layout */
         hipError_t e = fmgi_set_lds_attr_once<6>((const void *)k_bin, kBinBatch * 4);
         if (e != hipSuccess) return e;
         hipLaunchKernelGGL(k_bin, dim3((unsigned)std::max(1, sb.bin_grid)), dim3(kBinThreads), (size_t)kBinBatch * 4, s,
                            sb.dense, sb.cursor + 1, sb.dense_cap, P, sb.stream, sb.block_tile, sb.block_len, sb.cursor,
-                           sb.pool_blocks, (const uint4 *)sb.colpack, lm);
+                           sb.pool_blocks, (const uint4 *)sb.colpack, lm, (uint32_t)(10 + tb));
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
@@ -640,8 +643,10 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                                const uint4 *, unsigned long long *, int);
         static const FoldFn folds[] = {k_bucket_fold<0>, k_bucket_fold<1>, k_bucket_fold<2>, k_bucket_fold<3>,
                                        k_bucket_fold<4>};
-        const FoldFn fn = folds[exp >= 0 && exp <= 4 ? exp : 0];
+        const bool wide = sb.tile_bits == FMGI_WIDE_TILE_BITS && FMGI_WIDE_TILE_BITS != FMGI_TILE_BITS;
+        const FoldFn fn = wide ? (FoldFn)k_bucket_fold<0, FMGI_WIDE_TILE_BITS> : folds[exp >= 0 && exp <= 4 ? exp : 0];
         e = fn == folds[0] ? fmgi_set_lds_attr_once<3>((const void *)fn, (int)plds)
+            : wide         ? fmgi_set_lds_attr_once<7>((const void *)fn, (int)plds)
                            : hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;

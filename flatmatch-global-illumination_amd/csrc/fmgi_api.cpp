@@ -923,17 +923,33 @@ static uint64_t stream_alloc_codes(uint64_t cap, int P, int grid, int block, int
     return mode >= kStreamBuckets ? bucket_pool_blocks(cap, P, grid, block) * FMGI_BUCKET_BLOCK : cap;
 }
 
+/* fold tiles of 2^bits texels over the lightmap */
+static int tiles_of(const fmgi_context *c, int bits) { return (c->num_texels + (1 << bits) - 1) >> bits; }
+
+/* The fold tile of a STREAM chunk: 2048 texels (FMGI_TILE_BITS), or 4096 (FMGI_WIDE_TILE_BITS) in the bucket
+   layouts when the chunk is large. Wide tiles halve the tiles, so each wave-iteration's deposit stores touch
+   ~22 instead of ~34 lines (box200 bake 65.7 -> 60.8 ms), while the fold's 96-KB accumulators run one
+   workgroup per CU (fold +1.2 ms whatever the chunk: example.png's 1e8 photons lose overall, 22.6 -> 23.2 ms;
+   profiles/r05/s16). So: wide from 3e6 work items (3e8 photons) per chunk. FMGI_WIDE_TILES=0/1 forces. */
+static int tile_bits(const fmgi_context *c, int mode, uint64_t items) {
+    if (mode < kStreamBuckets) return FMGI_TILE_BITS;
+    if (const char *we = getenv("FMGI_WIDE_TILES")) return atoi(we) == 1 ? FMGI_WIDE_TILE_BITS : FMGI_TILE_BITS;
+    return items >= 3000000 ? FMGI_WIDE_TILE_BITS : FMGI_TILE_BITS;
+}
+
 static bool ensure_stream_needs_growth(const fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
-    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
+    const int P = tiles_of(c, FMGI_TILE_BITS);
     return stream_alloc_codes(stream_cap_for(items, grid, block), P, grid, block, mode) > c->sb_cap_alloc[k] ||
            (mode == kStreamSliced && !c->sb[k].sorted) ||
            (mode == kStreamDense && dense_cap_for(items, grid, block) > c->sb[k].dense_alloc);
 }
 
-static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block, int mode) {
+static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int block, int mode, int tbits) {
     StreamBufs &sb = c->sb[k];
     const uint64_t cap = stream_cap_for(items, grid, block);
-    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
+    /* (the pool is sized for the narrow tiles' open blocks: enough for either) */
+    const int P = tiles_of(c, FMGI_TILE_BITS);
+    sb.tile_bits = tbits;
     const uint64_t codes = stream_alloc_codes(cap, P, grid, block, mode);
     if (codes > c->sb_cap_alloc[k] || (mode == kStreamSliced && !sb.sorted)) {
         hipFree(sb.stream);
@@ -992,6 +1008,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
        tiles, presorted: 19.6 / 18.9 / 17.4 / 16.5 ms at 11 / 22 / 45 / 90 groups) */
     {
         const int ncu = std::max(1, c->num_cus);
+        const int Pf = tiles_of(c, mode >= kStreamBuckets ? tbits : FMGI_TILE_BITS); /* the fold's tiles */
         const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
         /* bucketed: ~36 rounds (box200, 46 tiles: fold 11.22 / 10.86 / 10.92 / 11.19 / 12.70 ms at 96 / 200 /
            300 / 800 / 1600 groups, profiles/r03/s21-s22: finer shares of the largest tiles against the
@@ -999,7 +1016,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         /* slice-sorted (lightmaps of more than 63 tiles): ~48 rounds (30-room layout, 358 tiles: fold 7.49 /
            7.31 / 6.34 / 5.97 ms at 8 / 4 / 16 / 32 groups per tile, profiles/r03/s33) */
         const int rounds = mode >= kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 48);
-        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + P - 1) / P);
+        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + Pf - 1) / Pf);
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
            or 16 chain blocks (one per wave), per workgroup */
@@ -1008,7 +1025,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups, std::max<uint64_t>(8, cap / FMGI_RING_CODES / 1024));
             if (mode >= kStreamBuckets) /* at least one 4-KB block per wave of every workgroup */
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
-                                                    std::max<uint64_t>(8, (cap / FMGI_BUCKET_BLOCK) / ((uint64_t)P * 16)));
+                                                    std::max<uint64_t>(8, (cap / FMGI_BUCKET_BLOCK) / ((uint64_t)Pf * 16)));
             if (mode == kStreamSliced) /* at least one big slice's worth of codes per workgroup and tile */
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
                                                     std::max<uint64_t>(8, cap / ((uint64_t)P * FMGI_STREAM_SLICE_BIG)));
@@ -1884,7 +1901,6 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const int lanes = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, UINT64_MAX) * block;
     int pipeline = 1;
     if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
-    const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
     const int smode = stream_layout(c); /* kStreamBuckets <=> kacc == kAccBucket */
     uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, smode);
     if (const char *ce = getenv("FMGI_CHUNK_ITEMS")) /* tests: force several chunks */
@@ -1913,7 +1929,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             HIPCHK(hipStreamSynchronize(s));
             if (c->fold_stream) HIPCHK(hipStreamSynchronize(c->fold_stream));
         }
-        int rc = ensure_stream(c, k, ce - cb, grid, block, smode);
+        const int tbits = tile_bits(c, smode, ce - cb);
+        int rc = ensure_stream(c, k, ce - cb, grid, block, smode, tbits);
         if (rc != FMGI_OK) return rc;
         StreamBufs &sb = c->sb[k];
         a.item_begin = cb;
@@ -1922,7 +1939,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.stream_cap = sb.cap;
         a.stream_cursor = sb.cursor;
         a.presort = smode;
-        a.ntiles = P;
+        a.ntiles = tiles_of(c, tbits);
+        a.tile_shift = 10 + tbits;
         a.toff = sb.toff;
         a.colpack = (const uint4 *)c->d_colpack;
         if (smode == kStreamBuckets) {

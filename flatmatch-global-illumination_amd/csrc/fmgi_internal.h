@@ -138,6 +138,7 @@ struct BakeArgs {
     unsigned long long *pool_cursor;
     uint64_t pool_blocks;
     const uint4 *colpack; /* {R, G - R, B - R, 0} per colour state (the bucketed stream's atomic fallback) */
+    int tile_shift;       /* a code's fold tile is code >> tile_shift (10 + tile bits: 11, or 12 for wide tiles) */
     int ring_off;                 /* byte offset of the per-wave code rings in dynamic LDS (fmgi_bake_lds) */
     int num_texels;
     /* debug trace (TRACE kernels only) */
@@ -174,9 +175,13 @@ static_assert(FMGI_STREAM_SLICE_BIG % FMGI_STREAM_SLICE == 0, "run tables are si
 #ifndef FMGI_BUCKET_ALLOC         /* pool blocks a wave reserves at a time (experiment builds)   */
 #define FMGI_BUCKET_ALLOC 8
 #endif
+#ifndef FMGI_TILE_BITS          /* (experiment builds: make fullvariant VFLAGS=-DFMGI_TILE_BITS=12) */
 #define FMGI_TILE_BITS 11      /* 2048-texel tiles summed in LDS (64 KB: two sum workgroups per
                                   CU; measured 25 ms per 1e9 photons vs 28 ms with 4096, 31 ms with 1024) */
-#define FMGI_MAX_TILES 2048    /* => at most 4M texels (and texel < 2^22 keeps codes != ~0u)   */
+#endif
+#define FMGI_MAX_TILES (1 << (22 - FMGI_TILE_BITS)) /* => at most 4M texels (texel < 2^22 keeps codes != ~0u) */
+#define FMGI_WIDE_TILE_BITS 12 /* the bucket layouts' wide fold tiles (4096 texels, 96 KB of accumulators): half
+                                  the tiles, so a wave's deposit stores touch fewer lines (fmgi_api.cpp tile_bits) */
 
 struct StreamBufs {
     uint32_t *stream;           /* deposit codes, cap entries                                   */
@@ -200,6 +205,8 @@ struct StreamBufs {
     uint32_t *dense;
     uint64_t dense_cap, dense_alloc;
     int bin_grid;                     /* k_bin workgroups (persistent: two per CU)                     */
+    int tile_bits;                    /* fold tile = 2^tile_bits texels: FMGI_TILE_BITS, or 12 (wide tiles,
+                                         bucket layouts only)                                           */
 };
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);
 

@@ -1094,7 +1094,7 @@ struct AccStreamT {
         const uint32_t nl = (uint32_t)__popcll(live);
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
         const int P = uni(a.ntiles);
-        const uint32_t shift = 10 + FMGI_TILE_BITS;
+        const uint32_t shift = (uint32_t)uni(a.tile_shift);
         for (uint32_t k = r; k < 64; k += nl) hist[k] = 0;
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1300,7 +1300,7 @@ struct AccStreamT {
         const uint32_t nl = (uint32_t)__popcll(live);
         const uint32_t r = __builtin_amdgcn_mbcnt_hi((uint32_t)(live >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)live, 0u));
         const int P = uni(a.ntiles);
-        const uint32_t shift = 10 + FMGI_TILE_BITS;
+        const uint32_t shift = (uint32_t)uni(a.tile_shift);
         for (uint32_t t = r; t < 64; t += nl) hist[t] = 0;
         __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -1601,7 +1601,7 @@ struct AccLines {
     static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &, uint32_t *base, bool dep,
                                                   uint32_t code) {
         if (__ballot(dep) == 0) return;
-        const uint32_t t = code >> (10 + FMGI_TILE_BITS);
+        const uint32_t t = code >> uni(a.tile_shift);
         uint32_t old = 0;
         if (dep) old = __hip_atomic_fetch_add(ctr(base) + t, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         bool pend = dep;
@@ -1713,7 +1713,7 @@ struct AccScatter {
     static __device__ __forceinline__ void append(const BakeArgs &a, WaveStream &, uint32_t *base, bool dep,
                                                   uint32_t code) {
         u64 *T = tab(base);
-        const uint32_t t = code >> (10 + FMGI_TILE_BITS);
+        const uint32_t t = code >> uni(a.tile_shift);
 #if defined(FMGI_SCATTER_EXP) && FMGI_SCATTER_EXP == 2 /* PROFILING ONLY: no slot, no store; the codes xor-ed */
         if (dep) T[64 + (threadIdx.x & 63)] ^= code; /* (a per-lane LDS word past the table: keeps the code live) */
         return;
@@ -1814,7 +1814,7 @@ struct AccDense {
         uint64_t dst = base + (BLK - room) + r;
         if (n > room) { /* (uniform) the block fills: the rest of the codes start the next one */
             unsigned long long nb = 0;
-            if (r == 0) { /* (the first depositing lane) */
+            if (dep && r == 0) { /* the first depositing lane (a lane below it that does not deposit has r == 0 too) */
                 nb = atomicAdd(a.stream_cursor, (unsigned long long)BLK);
                 if (nb + BLK > a.stream_cap) atomicAdd(a.overflow, 1ull);
             }
@@ -1943,27 +1943,6 @@ __device__ __forceinline__ SrcDev load_src(const BakeArgs &a, const char *lds, i
     return src_fields(((gptr<SrcDev>)a.srcs)[srci]);
 }
 
-/* The sampler basis of a diffuse bounce (photonmap.cl:238 on the rect just hit): re-read from the rect table
-   at the top of the next iteration, from the workgroup's LDS copy when staged (BakeArgs::rects_off), instead of
-   being held in nine registers across the scan. FMGI_BASIS_RELOAD=0 builds keep the registers. */
-#ifndef FMGI_BASIS_RELOAD
-#define FMGI_BASIS_RELOAD 0
-#endif
-__device__ __forceinline__ void load_basis(const BakeArgs &a, const char *lds, int idx, f3 &n, f3 &bu, f3 &bv) {
-    if (uni(a.rects_off) >= 0) {
-        const __attribute__((address_space(3))) RectLds &r = *(const __attribute__((address_space(3))) RectLds *)(
-            (const __attribute__((address_space(3))) char *)lds + a.rects_off + __umul24((uint32_t)idx, (uint32_t)sizeof(RectLds)));
-        n = mkf3(r.nx, r.ny, r.nz);
-        bu = mkf3(r.bux, r.buy, r.buz);
-        bv = mkf3(r.bvx, r.bvy, r.bvz);
-    } else {
-        const gptr<RectDev> r = ((gptr<RectDev>)a.rects) + idx;
-        n = mkf3(r->nx, r->ny, r->nz);
-        bu = mkf3(r->bux, r->buy, r->buz);
-        bv = mkf3(r->bvx, r->bvy, r->bvz);
-    }
-}
-
 /* LCG^2: the two draws of a direction sample whose result is never used (last bounce) */
 __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
     constexpr uint32_t A2 = kJump.a[2], C2 = kJump.c[2];
@@ -2011,9 +1990,6 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     uint32_t rng = 0;
     f3 pos = mkf3(0, 0, 0), dir = mkf3(0, 0, 0), col = mkf3(0, 0, 0);
     f3 sn = mkf3(0, 0, 0), sbu = mkf3(0, 0, 0), sbv = mkf3(0, 0, 0); /* pending diffuse sample basis */
-#if FMGI_BASIS_RELOAD
-    int bidx = 0; /* the rect of the pending diffuse sample */
-#endif
     int depth = 0, left = 0, photon = -1, sid = 0, srci = 0;
     bool win = false, start = true, pend = false;
     uint64_t item = 0;
@@ -2094,9 +2070,6 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
             n_ph++;
         }
         sst.clk.lap(ST_START);
-#if FMGI_BASIS_RELOAD
-        if (!start && pend) load_basis(a, s_img, bidx, sn, sbu, sbv); /* the last hit's rect */
-#endif
         if (start || pend) dir = sample_dir(rng, sn, sbu, sbv, start && win);
         if (start) {
             const SrcDev S = load_src<ScanStaged<Scan>::value>(a, s_img, srci);
@@ -2118,13 +2091,9 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         uint32_t code = 0;
         /* the basis of a diffuse sample at the top of the next iteration (unused unless pend is set; an
            escaped photon's next sample is an emission, whose basis the start block sets) */
-#if FMGI_BASIS_RELOAD
-        bidx = h.idx; /* (re-read there: one register held across the iteration instead of nine) */
-#else
         sn = mkf3(h.nx, h.ny, h.nz);
         sbu = mkf3(h.bux, h.buy, h.buz);
         sbv = mkf3(h.bvx, h.bvy, h.bvz);
-#endif
         if (h.best == INFINITY) { /* photonmap.cl:208-209 */
             start = true;
             n_esc++;
