@@ -284,6 +284,9 @@ typedef float pkf2 __attribute__((ext_vector_type(2)));
 #ifndef FMGI_FILTER_PK
 #define FMGI_FILTER_PK 1
 #endif
+#ifndef FMGI_PAIR_PREFETCH
+#define FMGI_PAIR_PREFETCH 1
+#endif
 
 __device__ __forceinline__ void pair_rec(float f, float uu, float vv, float hu, float hv, int idx, float &L1,
                                          float &L2, int &code1) {
@@ -306,16 +309,32 @@ __device__ __forceinline__ void filter_pairs(const char *img, int G, f3 s, f3 d,
     const pkf2 su2 = {comp<U>(s), comp<U>(s)}, sv2 = {comp<V>(s), comp<V>(s)};
     const pkf2 du2 = {comp<U>(d), comp<U>(d)}, dv2 = {comp<V>(d), comp<V>(d)};
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + (da < 0.0f ? 0 : 48), 16);
-#pragma unroll 2
-    for (int g = 0; g < G; g++) {
-        const float4 q0 = p[6 * g], q1 = p[6 * g + 1], q2 = p[6 * g + 2];
+    auto group = [&](float4 q0, float4 q1, float4 q2) {
         const pkf2 pl = {q0.x, q0.y}, cu = {q0.z, q0.w}, cv = {q1.z, q1.w};
         const pkf2 f = (pl - sa2) * rd2;
         const pkf2 uu = __builtin_elementwise_fma(du2, f, su2) - cu;
         const pkf2 vv = __builtin_elementwise_fma(dv2, f, sv2) - cv;
         pair_rec(f.x, uu.x, vv.x, q1.x, q2.x, __float_as_int(q2.z), L1, L2, code1);
         pair_rec(f.y, uu.y, vv.y, q1.y, q2.y, __float_as_int(q2.w), L1, L2, code1);
+    };
+#if FMGI_PAIR_PREFETCH
+    /* two groups per iteration with all six reads issued first (left to itself, the scheduler waits
+       for each group's reads right after issuing them, exposing the LDS latency once per group;
+       example.png bake 21.07 -> 20.78 ms, profiles/r05/s20) */
+    int g = 0;
+    for (; g + 1 < G; g += 2) {
+        const float4 a0 = p[6 * g], a1 = p[6 * g + 1], a2 = p[6 * g + 2];
+        const float4 b0 = p[6 * g + 6], b1 = p[6 * g + 7], b2 = p[6 * g + 8];
+        __builtin_amdgcn_sched_group_barrier(0x100, 6, 0);
+        __builtin_amdgcn_sched_group_barrier(0x00F, 400, 0);
+        group(a0, a1, a2);
+        group(b0, b1, b2);
     }
+    if (g < G) group(p[6 * g], p[6 * g + 1], p[6 * g + 2]);
+#else
+#pragma unroll 2
+    for (int g = 0; g < G; g++) group(p[6 * g], p[6 * g + 1], p[6 * g + 2]);
+#endif
 }
 
 /* merges the phase-1 results (L1, L2, code1) of the coop lanes of a group (butterfly over lane ids):
