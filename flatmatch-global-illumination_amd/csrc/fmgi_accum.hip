@@ -328,7 +328,13 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
    was slower. */
 /* 8 waves per SIMD (<= 64 VGPRs): two 1024-lane workgroups per CU, as their 64 KB of LDS allow (at 66
    VGPRs only one fitted, and the fold took 13.7 ms instead of 11) */
-template <int EXP, int TB = FMGI_TILE_BITS>
+/* SPLIT > 1: the buckets' tiles are SPLIT fold tiles wide (bucket tile bits = TB + log2 SPLIT); each
+   (tile, group of blocks) gets SPLIT workgroups, one per fold tile, that read the same blocks and sum only
+   their own texels' codes. The SPLIT workgroups of one block range are dispatched 8 apart, i.e. on one XCD
+   at about the same time, so the blocks' second and later reads are meant to hit its L2 (or the Infinity
+   Cache) rather than HBM. The bake's per-lane bucket stores touch fewer lines per store the wider its
+   tiles (§4.1), while the fold keeps 64-KB workgroups, two per CU. */
+template <int EXP, int TB = FMGI_TILE_BITS, int SPLIT = 1>
 __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restrict__ pool,
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ block_len,
@@ -337,6 +343,12 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
                                                      unsigned long long *__restrict__ lm, int num_texels) {
     constexpr uint32_t BP = FMGI_BUCKET_BLOCK;
     constexpr int kTileTexels = 1 << TB; /* this instance's fold tile */
+    constexpr int kSplitBits = SPLIT == 4 ? 2 : (SPLIT == 2 ? 1 : 0);
+    static_assert(SPLIT == 1 << kSplitBits, "SPLIT must be 1, 2 or 4");
+    constexpr uint32_t kBucketMask = (1u << (TB + kSplitBits)) - 1; /* texel bits of a bucket tile */
+    const uint32_t n = blockIdx.x;
+    const uint32_t part = SPLIT > 1 ? (n >> 3) & (SPLIT - 1) : 0u;                   /* fold tile in the bucket */
+    const uint32_t wid = SPLIT > 1 ? ((n >> (3 + kSplitBits)) << 3) | (n & 7) : n; /* the block-range workgroup */
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
     unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
     uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
@@ -345,7 +357,7 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
         /* the P * G workgroups shared out in proportion to the tiles' block counts (at least one each):
            tile t owns workgroups [c(t), c(t + 1)) with c(t) = t + floor((W - P) * blocks before t / all),
            so every workgroup folds about the same number of blocks whatever the tiles' sizes */
-        const uint32_t W = (uint32_t)(P * G), w = blockIdx.x;
+        const uint32_t W = (uint32_t)(P * G), w = wid;
         uint64_t total = 0;
         for (int u = 0; u < P; u++) total += counts[u];
         if (total == 0) return;
@@ -367,7 +379,7 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
         j_lo = (uint32_t)((uint64_t)nt * g / wt);
         j_hi = (uint32_t)((uint64_t)nt * (g + 1) / wt);
     } else {
-        const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
+        const int xcd = (int)(wid & 7), j = (int)(wid >> 3); /* XCD-aware order, as k_tile_runs */
         t = (uint32_t)(j % P);
         const uint32_t g = (uint32_t)(xcd + 8 * (j / P));
         for (uint32_t u = 0; u < t; u++) off += counts[u];
@@ -422,6 +434,7 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
                 for (int m = 0; m < 4; m++) {
                     const uint32_t c = cs[m];
                     if (i0 + m >= len || c == kSentinel) continue; /* runs are padded to 4 codes */
+                    if (SPLIT > 1 && (((c >> 10) & kBucketMask) >> TB) != part) continue; /* another fold tile's */
                     const int tx = (int)((c >> 10) & (kTileTexels - 1));
                     if (EXP == 1) {
                         if (c == 0x7FFFFFFFu) acc_r[tx] = 1; /* never: keeps the loads */
@@ -446,7 +459,7 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
-        const int texel = t * kTileTexels + i;
+        const int texel = (int)((t << (TB + kSplitBits)) + part * kTileTexels) + i;
         if (texel >= num_texels) break;
         const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
         unsigned long long *qq = lm + 4 * (size_t)texel;
@@ -613,11 +626,25 @@ __global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restri
 
 } // namespace
 
+/* fold tiles per bucket tile for a bucket layout of 2^tb-texel tiles: FMGI_FOLD_SPLIT (1, 2 or 4) if set and
+   an instance exists, else 1 */
+int fmgi_fold_split(int tb) {
+    const char *e = getenv("FMGI_FOLD_SPLIT");
+    const int env = e ? atoi(e) : 0;
+    const int want = env > 0 ? env : FMGI_FOLD_SPLIT_DEFAULT;
+    if (tb == 12 && (want == 1 || want == 2)) return want;
+    if (tb == 13) return want == 4 ? 4 : 2; /* 8192-texel fold tiles do not fit LDS */
+    return 1;
+}
+
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s) {
     /* the bucket layouts' tiles may be wide (sb.tile_bits); the others are FMGI_TILE_BITS */
     const int tb = sb.presort >= 2 && sb.tile_bits > 0 ? sb.tile_bits : FMGI_TILE_BITS;
     const int P = (num_texels + (1 << tb) - 1) >> tb;
-    const size_t plds = (size_t)3 * ((size_t)1 << tb) * 8 + (size_t)FMGI_COLOUR_STATES * 16;
+    /* the bucket layouts' fold tiles: a bucket tile split in `split` fold tiles (fmgi_fold_split) */
+    const int split = sb.presort >= 2 ? fmgi_fold_split(tb) : 1;
+    const int fb = tb - (split == 4 ? 2 : split == 2 ? 1 : 0);
+    const size_t plds = (size_t)3 * ((size_t)1 << fb) * 8 + (size_t)FMGI_COLOUR_STATES * 16;
     if (sb.presort == 3) { /* the dense stream: binned into the pool, then folded as the bucket layout */
         hipError_t e = fmgi_set_lds_attr_once<6>((const void *)k_bin, kBinBatch * 4);
         if (e != hipSuccess) return e;
@@ -643,16 +670,24 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                                const uint4 *, unsigned long long *, int);
         static const FoldFn folds[] = {k_bucket_fold<0>, k_bucket_fold<1>, k_bucket_fold<2>, k_bucket_fold<3>,
                                        k_bucket_fold<4>};
-        const bool wide = sb.tile_bits == FMGI_WIDE_TILE_BITS && FMGI_WIDE_TILE_BITS != FMGI_TILE_BITS;
-        const FoldFn fn = wide ? (FoldFn)k_bucket_fold<0, FMGI_WIDE_TILE_BITS> : folds[exp >= 0 && exp <= 4 ? exp : 0];
-        e = fn == folds[0] ? fmgi_set_lds_attr_once<3>((const void *)fn, (int)plds)
-            : wide         ? fmgi_set_lds_attr_once<7>((const void *)fn, (int)plds)
-                           : hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+        FoldFn fn = nullptr;
+        if (tb == FMGI_TILE_BITS && split == 1) fn = folds[exp >= 0 && exp <= 4 ? exp : 0];
+        else if (tb == 12 && split == 1) fn = k_bucket_fold<0, 12, 1>;
+        else if (tb == 12 && split == 2) fn = k_bucket_fold<0, 11, 2>;
+        else if (tb == 13 && split == 2) fn = k_bucket_fold<0, 12, 2>;
+        else if (tb == 13 && split == 4) fn = k_bucket_fold<0, 11, 4>;
+        else return hipErrorInvalidValue; /* no instance for this tile width and split */
+        e = fn == folds[0]                            ? fmgi_set_lds_attr_once<3>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, 12, 1> ? fmgi_set_lds_attr_once<7>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, 11, 2> ? fmgi_set_lds_attr_once<8>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, 12, 2> ? fmgi_set_lds_attr_once<9>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, 11, 4> ? fmgi_set_lds_attr_once<10>((const void *)fn, (int)plds)
+                                                    : hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
         const char *be = getenv("FMGI_FOLD_BALANCE"); /* experiments: 0 = equal groups per tile */
         const int balanced = be ? atoi(be) != 0 : 1;
-        const dim3 grid((unsigned)(P * G)), blk(sb.block > 0 ? sb.block : 1024);
+        const dim3 grid((unsigned)(P * G * split)), blk(sb.block > 0 ? sb.block : 1024);
         hipLaunchKernelGGL(fn, grid, blk, plds, s, sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G,
                            balanced, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();

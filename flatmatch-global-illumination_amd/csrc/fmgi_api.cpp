@@ -933,7 +933,10 @@ static int tiles_of(const fmgi_context *c, int bits) { return (c->num_texels + (
    profiles/r05/s16). So: wide from 3e6 work items (3e8 photons) per chunk. FMGI_WIDE_TILES=0/1 forces. */
 static int tile_bits(const fmgi_context *c, int mode, uint64_t items) {
     if (mode < kStreamBuckets) return FMGI_TILE_BITS;
-    if (const char *we = getenv("FMGI_WIDE_TILES")) return atoi(we) == 1 ? FMGI_WIDE_TILE_BITS : FMGI_TILE_BITS;
+    if (const char *we = getenv("FMGI_WIDE_TILES")) { /* 0 / 1 (= 12) or the tile bits, 11-13 */
+        const int v = atoi(we);
+        return v == 1 ? FMGI_WIDE_TILE_BITS : (v >= 11 && v <= 13 ? v : FMGI_TILE_BITS);
+    }
     return items >= 3000000 ? FMGI_WIDE_TILE_BITS : FMGI_TILE_BITS;
 }
 
@@ -1016,7 +1019,9 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
         /* slice-sorted (lightmaps of more than 63 tiles): ~48 rounds (30-room layout, 358 tiles: fold 7.49 /
            7.31 / 6.34 / 5.97 ms at 8 / 4 / 16 / 32 groups per tile, profiles/r03/s33) */
         const int rounds = mode >= kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 48);
-        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + Pf - 1) / Pf);
+        /* (a split bucket tile gets `split` workgroups per group: the same rounds over the fold tiles) */
+        const int split = mode >= kStreamBuckets ? fmgi_fold_split(tbits) : 1;
+        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + Pf * split - 1) / (Pf * split));
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
            or 16 chain blocks (one per wave), per workgroup */

@@ -180,8 +180,13 @@ static_assert(FMGI_STREAM_SLICE_BIG % FMGI_STREAM_SLICE == 0, "run tables are si
                                   CU; measured 25 ms per 1e9 photons vs 28 ms with 4096, 31 ms with 1024) */
 #endif
 #define FMGI_MAX_TILES (1 << (22 - FMGI_TILE_BITS)) /* => at most 4M texels (texel < 2^22 keeps codes != ~0u) */
-#define FMGI_WIDE_TILE_BITS 12 /* the bucket layouts' wide fold tiles (4096 texels, 96 KB of accumulators): half
-                                  the tiles, so a wave's deposit stores touch fewer lines (fmgi_api.cpp tile_bits) */
+#define FMGI_WIDE_TILE_BITS 12 /* the bucket layouts' wide tiles (4096 texels): half the tiles, so a wave's
+                                  deposit stores touch fewer lines (fmgi_api.cpp tile_bits) */
+#ifndef FMGI_FOLD_SPLIT_DEFAULT  /* fold tiles per wide bucket tile (fmgi_fold_split): 1 = one
+                                    4096-texel fold (96 KB of accumulators, one workgroup per CU), 2 = two
+                                    2048-texel folds reading the same blocks */
+#define FMGI_FOLD_SPLIT_DEFAULT 1
+#endif
 
 struct StreamBufs {
     uint32_t *stream;           /* deposit codes, cap entries                                   */
@@ -205,10 +210,11 @@ struct StreamBufs {
     uint32_t *dense;
     uint64_t dense_cap, dense_alloc;
     int bin_grid;                     /* k_bin workgroups (persistent: two per CU)                     */
-    int tile_bits;                    /* fold tile = 2^tile_bits texels: FMGI_TILE_BITS, or 12 (wide tiles,
-                                         bucket layouts only)                                           */
+    int tile_bits;                    /* bucket tile = 2^tile_bits texels: FMGI_TILE_BITS, or 12-13 (wide
+                                         tiles, bucket layouts only; fold tiles per fold_split)         */
 };
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s);
+int fmgi_fold_split(int tile_bits); /* fold tiles per bucket tile of 2^tile_bits texels */
 
 #define FMGI_COLOUR_STATES 1024 /* bit 9: window (18,18,18) vs light (16,16,18); bits 0-8: 1 + diffuse-bounce floor bits */
 

@@ -178,6 +178,13 @@ FOLD_LAYOUTS = {  # stream layout -> the environment that selects it
     "buckets_scatter_wide": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_WIDE_TILES": "1"},
     "buckets_ring_wide": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "0", "FMGI_WIDE_TILES": "1"},
     "dense_bin_wide": {"FMGI_PRESORT": "2", "FMGI_DENSE": "1", "FMGI_WIDE_TILES": "1"},
+    # wide bucket tiles folded as 2 or 4 narrower fold tiles that read the same blocks
+    "buckets_scatter_wide_split2": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_WIDE_TILES": "1",
+                                    "FMGI_FOLD_SPLIT": "2"},
+    "buckets_scatter_w13_split2": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_WIDE_TILES": "13",
+                                   "FMGI_FOLD_SPLIT": "2"},
+    "buckets_ring_w13_split4": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "0", "FMGI_WIDE_TILES": "13",
+                                "FMGI_FOLD_SPLIT": "4"},
     "presorted": {"FMGI_PRESORT": "1"},
     "sliced": {"FMGI_PRESORT": "0", "FMGI_PACKED_RUNS": "0"},
     "sliced_packed": {"FMGI_PRESORT": "0", "FMGI_PACKED_RUNS": "1"},
@@ -197,8 +204,9 @@ def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, la
     63 fold tiles) filled through the bake's per-wave LDS rings (buckets_ring) or lane by lane (buckets_scatter),
     the bake's dense code stream binned into buckets by k_bin (dense_bin), the bake-side presorted segments, and
     the slice-sorted stream (its runs summed one at a time, or packed 16 slices to a wave as for lightmaps of more
-    than 128 tiles); the bucket layouts also with wide (4096-texel) fold tiles; for full-ring flushes and the
-    partial rings / blocks at the end of a launch."""
+    than 128 tiles); the bucket layouts also with wide (4096- or 8192-texel) tiles, folded whole or as 2 or 4
+    narrower fold tiles that each read every block of the bucket; for full-ring flushes and the partial rings /
+    blocks at the end of a launch."""
     _set_layout(layout)
     try:
         for sc, spa, lo, hi in ((box200, 172_413_793, 7_000, 27_000), (example_scene, 65_000, 0, 300)):
