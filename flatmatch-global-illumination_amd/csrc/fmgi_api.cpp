@@ -1018,7 +1018,10 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
            per-workgroup set-up and flush) */
         /* slice-sorted (lightmaps of more than 63 tiles): ~48 rounds (30-room layout, 358 tiles: fold 7.49 /
            7.31 / 6.34 / 5.97 ms at 8 / 4 / 16 / 32 groups per tile, profiles/r03/s33) */
-        const int rounds = mode >= kStreamBuckets ? 36 : (mode == kStreamSegments ? 16 : 48);
+        /* (wide bucket tiles: one 96-KB fold workgroup per CU instead of two, so half the rounds; box200 fold
+           11.93 / 11.58 / 11.91 ms at ~408 / 200 / 300 groups per tile, profiles/r05/s26-s27) */
+        const bool wide = mode >= kStreamBuckets && tbits > FMGI_TILE_BITS && fmgi_fold_split(tbits) == 1;
+        const int rounds = mode >= kStreamBuckets ? (wide ? 18 : 36) : (mode == kStreamSegments ? 16 : 48);
         /* (a split bucket tile gets `split` workgroups per group: the same rounds over the fold tiles) */
         const int split = mode >= kStreamBuckets ? fmgi_fold_split(tbits) : 1;
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + Pf * split - 1) / (Pf * split));
