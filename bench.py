@@ -277,7 +277,7 @@ def binding_of(issue, atomic_rate):
           "valu": issue.get("valu_frac_of_peak") or 0.0}
     res = max(fr, key=fr.get)
     w = issue["wave_cycles"]
-    if fr[res] >= 0.85:
+    if fr[res] >= 0.8:  # (box200's VALU issue: 84 % of the ceiling 6 waves per SIMD reach, profiles/r05/s23)
         what = {"vmem": "vector-memory path (TA/TD busy %.0f %% of cycles)" % (100 * fr["vmem"]),
                 "valu": "VALU issue (%.0f %% of the measured ceiling)" % (100 * fr["valu"])}[res]
         return res, what + "; waves parked on s_waitcnt %.0f %% of wave cycles" % (100 * w["waiting"])
