@@ -185,6 +185,9 @@ struct ScanStats {
     uint32_t invalid = 0; /* the phase-1 winner failed the exact test     */
 };
 
+#ifndef FMGI_LITERAL_LDS /* the fallbacks' literal scan reads the staged walls from LDS (0: the global table) */
+#define FMGI_LITERAL_LDS 1
+#endif
 /* photonmap.cl:189-206, evaluated literally for every rectangle in index order. */
 struct ScanExact {
     static constexpr bool kLds = false;
@@ -198,12 +201,31 @@ struct ScanExact {
     }
     /* Scalar: records through scalar loads (the exact kernel's own uniform loop); else vector loads (the
        other scans' rare fallback) */
-    template <bool Scalar = false>
-    static __device__ __forceinline__ int literal(const BakeArgs &a, const char *, f3 src, f3 dir, float &best,
+    template <bool Scalar = false, bool Staged = false>
+    static __device__ __forceinline__ int literal(const BakeArgs &a, const char *lds, f3 src, f3 dir, float &best,
                                                   ScanStats &st) {
         cptr<RectDev> R = (cptr<RectDev>)a.rects;
         float bestd = INFINITY;
         int hit = -1;
+#if FMGI_LITERAL_LDS
+        if (Staged || (!Scalar && uni(a.rects_off) >= 0)) {
+            /* the walls staged in LDS (RectLds): every lane of the wave reads the same record (a broadcast),
+               where the global table costs a dependent L2 round trip per rect */
+            const __attribute__((address_space(3))) char *l = (const __attribute__((address_space(3))) char *)lds;
+            for (int i = 0; i < uni(a.nrects); i++) {
+                const __attribute__((address_space(3))) RectLds &r =
+                    *(const __attribute__((address_space(3))) RectLds *)(l + a.rects_off + i * (int)sizeof(RectLds));
+                const float d = intersect_exact(mkf3(r.nx, r.ny, r.nz), mkf3(r.px, r.py, r.pz),
+                                                mkf3(r.wnx, r.wny, r.wnz), r.wl, mkf3(r.hnx, r.hny, r.hnz), r.hl, src,
+                                                dir, bestd);
+                if (d < 0) continue;
+                if (d < bestd) { bestd = d; hit = i; }
+            }
+            st.tests += (uint32_t)a.nrects;
+            best = bestd;
+            return hit;
+        }
+#endif
         for (int i = 0; i < uni(a.nrects); i++) {
             const float d = Scalar ? exact_on(R, i, src, dir, bestd) : exact_on_v(a.rects, i, src, dir, bestd);
             if (d < 0) continue;
@@ -875,7 +897,7 @@ struct ScanGridT {
         if (f < 0) st.invalid++; else st.ties++;
         float best;
         int r = ordered_exact(a, lds, src, dir, best);
-        if (r == -2) r = ScanExact::literal(a, lds, src, dir, best, st);
+        if (r == -2) r = ScanExact::literal<false, Staged>(a, lds, src, dir, best, st);
         finish_hit(a, r, best, src, dir, h);
         st.clk.lap(ST_FALLBACK);
     }
