@@ -271,6 +271,18 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
    whole 4-KB block (16 codes per lane, four 16-B loads, all in flight before the first add) and sums it
    exactly in LDS as k_tile_runs does. */
 constexpr int kListThreads = 1024;
+
+/* k_bucket_fold's CARRY channels: value v (a u32 two's complement int32) added to lo[tx]; hi[tx] (at lo + T)
+   takes the carry or borrow of the 64-bit sum */
+__device__ __forceinline__ void carry_add(uint32_t *lo, int T, int tx, uint32_t v) {
+    const uint32_t old = atomicAdd(&lo[tx], v); /* ds_add_rtn_u32 */
+    const uint32_t nw = old + v;
+    const int delta = (int)(nw < old) - (int)((int32_t)v < 0);
+    if (delta) atomicAdd(&lo[T + tx], (uint32_t)delta);
+}
+__device__ __forceinline__ unsigned long long carry_val(const uint32_t *lo, int T, int i) {
+    return ((unsigned long long)lo[T + i] << 32) | lo[i];
+}
 constexpr int kListPerThread = 8;
 
 __global__ __launch_bounds__(kListThreads) void k_bucket_count(const uint32_t *__restrict__ block_tile,
@@ -334,7 +346,13 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
    at about the same time, so the blocks' second and later reads are meant to hit its L2 (or the Infinity
    Cache) rather than HBM. The bake's per-lane bucket stores touch fewer lines per store the wider its
    tiles (§4.1), while the fold keeps 64-KB workgroups, two per CU. */
-template <int EXP, int TB = FMGI_TILE_BITS, int SPLIT = 1>
+/* CARRY: channels summed as a u32 low word with a returning ds_add_rtn_u32 plus a u32 carry
+   word that takes +-1 only when the low word wraps (old + v < old for v >= 0; a negative difference borrows
+   when old + v >= old): 0 = every channel as one ds_add_u64 (default), 1 = G - R and B - R with carries
+   (their adds wrap ~1/64 of the time), 2 = R as well. The sum mod 2^64 is the same either way: a channel is
+   hi * 2^32 + lo, and only hi mod 2^32 matters mod 2^64. The carry channels reuse the u64 array's 8 B per texel
+   as lo[T] | hi[T]. */
+template <int EXP, int TB = FMGI_TILE_BITS, int SPLIT = 1, int CARRY = 0>
 __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restrict__ pool,
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ block_len,
@@ -446,8 +464,14 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
                     }
                     const uint4 cc = EXP == 4 ? make_uint4(c & 1023, (c & 3) ? c & 511 : 0u, (c & 3) ? c & 255 : 0u, 0u)
                                               : col[c & 1023];
-                    atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
+                    if (CARRY >= 2) carry_add((uint32_t *)acc_r, kTileTexels, tx, cc.x);
+                    else atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
                     if (EXP == 3) continue;
+                    if (CARRY >= 1) {
+                        if (cc.y) carry_add((uint32_t *)acc_g, kTileTexels, tx, cc.y);
+                        if (cc.z) carry_add((uint32_t *)acc_b, kTileTexels, tx, cc.z);
+                        continue;
+                    }
                     if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
                     if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
                 }
@@ -461,7 +485,10 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
     for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
         const int texel = (int)((t << (TB + kSplitBits)) + part * kTileTexels) + i;
         if (texel >= num_texels) break;
-        const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
+        const unsigned long long r = CARRY >= 2 ? carry_val((const uint32_t *)acc_r, kTileTexels, i) : acc_r[i];
+        const unsigned long long ag = CARRY >= 1 ? carry_val((const uint32_t *)acc_g, kTileTexels, i) : acc_g[i];
+        const unsigned long long ab = CARRY >= 1 ? carry_val((const uint32_t *)acc_b, kTileTexels, i) : acc_b[i];
+        const unsigned long long gg = r + ag, bb = r + ab;
         unsigned long long *qq = lm + 4 * (size_t)texel;
         if (r) atomicAdd(qq + 0, r);
         if (gg) atomicAdd(qq + 1, gg);
@@ -677,11 +704,22 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
         else if (tb == 13 && split == 2) fn = k_bucket_fold<0, 12, 2>;
         else if (tb == 13 && split == 4) fn = k_bucket_fold<0, 11, 4>;
         else return hipErrorInvalidValue; /* no instance for this tile width and split */
+        {
+            const char *ce = getenv("FMGI_FOLD_CARRY"); /* experiments: 1 = G/B, 2 = R/G/B carry words */
+            const int carry = ce ? atoi(ce) : 0;
+            const bool plain = split == 1 && (tb == 12 || exp == 0);
+            if (plain && carry == 1) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 1> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1>;
+            if (plain && carry == 2) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 2> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
+        }
         e = fn == folds[0]                            ? fmgi_set_lds_attr_once<3>((const void *)fn, (int)plds)
             : fn == (FoldFn)k_bucket_fold<0, 12, 1> ? fmgi_set_lds_attr_once<7>((const void *)fn, (int)plds)
             : fn == (FoldFn)k_bucket_fold<0, 11, 2> ? fmgi_set_lds_attr_once<8>((const void *)fn, (int)plds)
             : fn == (FoldFn)k_bucket_fold<0, 12, 2> ? fmgi_set_lds_attr_once<9>((const void *)fn, (int)plds)
             : fn == (FoldFn)k_bucket_fold<0, 11, 4> ? fmgi_set_lds_attr_once<10>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, 12, 1, 1> ? fmgi_set_lds_attr_once<11>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, 12, 1, 2> ? fmgi_set_lds_attr_once<12>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1> ? fmgi_set_lds_attr_once<13>((const void *)fn, (int)plds)
+            : fn == (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2> ? fmgi_set_lds_attr_once<14>((const void *)fn, (int)plds)
                                                     : hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;

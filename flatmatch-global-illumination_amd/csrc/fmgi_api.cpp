@@ -23,6 +23,7 @@
 #include <string.h>
 
 #include <algorithm>
+#include <map>
 #include <mutex>
 #include <string>
 #include <thread>
@@ -736,6 +737,13 @@ struct fmgi_context {
     uint64_t blob_key = ~0ull;
     std::vector<RectLds> h_rects_lds; /* host staging of the LDS rect copy (kept until the copy is done) */
     bool warned_cells = false;        /* the coarse LDS grid was launched unstaged (said once)          */
+    /* the compact closed-box tables (fmgi_internal.h RectC ...; build_compact): set when a closed box's
+       RectLds walls and 32-B cells do not fit LDS but these do; the grid is then the one they index */
+    bool compact = false;
+    std::vector<RectC> h_rectc;
+    std::vector<ClassC> h_classc;
+    std::vector<float> h_recf;     /* {cu, hwu, cv, hwv} by rect index, then the dummy */
+    std::vector<uint32_t> h_cellc; /* two u32 per cell: idx0 | idx1 << 16, idx2 | idx3 << 16 */
 };
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
@@ -1115,6 +1123,104 @@ static int fitting_kernel(const fmgi_context *c, int kernel, int accum, int bloc
     return FMGI_KERNEL_EXACT;
 }
 
+/* LDS a compact closed-box launch holds (one 1024-lane workgroup per CU): the scan image, the emitters, and the
+   compact tables, beside the lane-by-lane stores' tile words of its 16 waves */
+static size_t compact_bytes(int img_bytes, int nsrcs, size_t nclass, size_t nrects, size_t ncells) {
+    size_t off = ((size_t)img_bytes + 15) & ~(size_t)15;
+    off += (size_t)nsrcs * sizeof(SrcDev);
+    off += nclass * sizeof(ClassC);
+    off += (nrects * sizeof(RectC) + 15) & ~(size_t)15;
+    off += (nrects + 1) * 16;
+    off += ncells * 8;
+    return (off + 15) & ~(size_t)15;
+}
+static const size_t kCompactLds = 160 * 1024 - 16 * FMGI_SCATTER_STRIDE * 4;
+
+/* The compact tables of a closed box (ScanGridT's Compact instance) from the device-computed RectDev table, the
+   filter records and grid g: false if some limit does not hold (a cell of more than 4 records, 2^16 walls,
+   texel bases of 22 bits, 1024 classes, W or H of 16 bits) or a field does not round-trip bit for bit. */
+static bool build_compact(fmgi_context *c, const std::vector<RectDev> &rd, const FilterBuild &fb, const GridBuild &g) {
+    const size_t n = rd.size();
+    if (n == 0 || n >= 0xFFFF || !fb.general.empty()) return false;
+    std::vector<ClassC> cls;
+    std::map<std::vector<uint32_t>, uint32_t> key_of;
+    std::vector<RectC> rc(n);
+    auto bits = [](float x) { uint32_t b; memcpy(&b, &x, 4); return b; };
+    for (size_t i = 0; i < n; i++) {
+        const RectDev &r = rd[i];
+        if (r.base < 0 || r.base >= (1 << kCompactBaseBits) || r.W < 1 || r.W > 0xFFFF || r.H < 1 || r.H > 0xFFFF)
+            return false;
+        ClassC k;
+        memset(&k, 0, sizeof k);
+        k.nx = r.nx; k.ny = r.ny; k.nz = r.nz;
+        k.wnx = r.wnx; k.wny = r.wny; k.wnz = r.wnz;
+        k.hnx = r.hnx; k.hny = r.hny; k.hnz = r.hnz;
+        k.bux = r.bux; k.buy = r.buy; k.buz = r.buz;
+        k.bvx = r.bvx; k.bvy = r.bvy; k.bvz = r.bvz;
+        k.WH = r.W | (r.H << 16);
+        std::vector<uint32_t> key((const uint32_t *)&k, (const uint32_t *)&k + 16);
+        auto it = key_of.find(key);
+        uint32_t id;
+        if (it == key_of.end()) {
+            id = (uint32_t)cls.size();
+            if (id >= (uint32_t)kCompactMaxClasses) return false;
+            key_of.emplace(key, id);
+            cls.push_back(k);
+        } else {
+            id = it->second;
+        }
+        rc[i] = RectC{r.px, r.py, r.pz, r.wl, r.hl, (uint32_t)r.base | (id << kCompactBaseBits)};
+        /* the decode the kernel does (exact_hit_compact), compared bit for bit */
+        const ClassC &q = cls[rc[i].meta >> kCompactBaseBits];
+        const float got[] = {rc[i].px, rc[i].py, rc[i].pz, q.nx, q.ny, q.nz, q.wnx, q.wny, q.wnz, rc[i].wl, q.hnx, q.hny,
+                             q.hnz, rc[i].hl, q.bux, q.buy, q.buz, q.bvx, q.bvy, q.bvz};
+        const float want[] = {r.px, r.py, r.pz, r.nx, r.ny, r.nz, r.wnx, r.wny, r.wnz, r.wl, r.hnx, r.hny,
+                              r.hnz, r.hl, r.bux, r.buy, r.buz, r.bvx, r.bvy, r.bvz};
+        for (int f = 0; f < 20; f++)
+            if (bits(got[f]) != bits(want[f])) return false;
+        if ((int)(rc[i].meta & ((1u << kCompactBaseBits) - 1)) != r.base || (q.WH & 0xFFFF) != r.W ||
+            ((uint32_t)q.WH >> 16) != (uint32_t)r.H)
+            return false;
+    }
+    /* filter extents by rect index: every wall is a record of exactly one class list (no general rects) */
+    std::vector<float> recf((n + 1) * 4, 0.0f);
+    std::vector<char> seen(n, 0);
+    for (int a = 0; a < 3; a++)
+        for (int cl = 0; cl < 2; cl++)
+            for (const FilterRec &r : fb.cls[a][cl]) {
+                if (r.idx < 0 || (size_t)r.idx >= n || seen[(size_t)r.idx]) return false;
+                seen[(size_t)r.idx] = 1;
+                float *q = &recf[(size_t)r.idx * 4];
+                q[0] = r.cu; q[1] = r.hwu; q[2] = r.cv; q[3] = r.hwv;
+            }
+    for (size_t i = 0; i < n; i++)
+        if (!seen[i]) return false;
+    recf[n * 4 + 1] = -1.0f; /* the dummy: |x - 0| <= -1 never holds */
+    recf[n * 4 + 3] = -1.0f;
+    /* cells: up to four rect indices (inline two, then the overflow list), absent = the dummy */
+    const uint32_t D = (uint32_t)n;
+    std::vector<uint32_t> cellc(g.cells.size() * 2);
+    for (size_t ci = 0; ci < g.cells.size(); ci++) {
+        const GridCell &gc = g.cells[ci];
+        if (gc.count < 0 || gc.count > 4) return false;
+        uint32_t id[4] = {D, D, D, D};
+        for (int k = 0; k < gc.count; k++) {
+            const int32_t x = k == 0 ? gc.idx0 : k == 1 ? gc.idx1 : g.idx[(size_t)gc.rest + (size_t)k - 2];
+            if (x < 0 || (size_t)x >= n) return false;
+            id[k] = (uint32_t)x;
+        }
+        cellc[2 * ci] = id[0] | (id[1] << 16);
+        cellc[2 * ci + 1] = id[2] | (id[3] << 16);
+    }
+    if (compact_bytes((int)(g.img.size() * sizeof(GridPlane)), c->nsrcs, cls.size(), n, g.cells.size()) > kCompactLds)
+        return false;
+    c->h_rectc.swap(rc);
+    c->h_classc.swap(cls);
+    c->h_recf.swap(recf);
+    c->h_cellc.swap(cellc);
+    return true;
+}
+
 FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_walls, const fmgi_rect *windows,
                             int num_windows, const fmgi_rect *lights, int num_lights, int num_texels) {
     if (!c || num_walls < 0 || num_windows < 0 || num_lights < 0 || num_texels < 0 ||
@@ -1160,6 +1266,31 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
             }
         }
     }
+    /* closed boxes whose coarse cells do not fit either (BASELINE config 5): the finest grid of 4, 3 or 2 cells per
+       record with at most 4 records per cell whose compact tables fit (build_compact, after the device has
+       computed the walls' builtin-derived fields); FMGI_COMPACT=0 keeps the 16-per-record global grid */
+    GridBuild gcomp;
+    bool try_compact = false;
+    {
+        const char *ce = getenv("FMGI_COMPACT");
+        if (c->device != FMGI_HOST_ONLY && !c->cells_lds && !grid_cpr_env() && !(ce && atoi(ce) == 0) &&
+            gb.J[0] == 1 && gb.J[1] == 1 && gb.J[2] == 1 && !getenv("FMGI_NO_AXES") && fb.general.empty() &&
+            num_walls > 0 && num_walls < 0xFFFF) {
+            for (int cpr : {4, 3, 2}) {
+                GridBuild g = build_grid(fb, cpr);
+                bool ok = true;
+                for (const GridCell &gc : g.cells) ok = ok && gc.count <= 4;
+                /* (classes are at most a few per plane on a box; build_compact checks the real size) */
+                if (ok && compact_bytes((int)(g.img.size() * sizeof(GridPlane)), num_windows + num_lights, 64,
+                                        (size_t)num_walls, g.cells.size()) <= kCompactLds) {
+                    gcomp = g;
+                    try_compact = true;
+                    break;
+                }
+            }
+        }
+    }
+    c->compact = false;
     for (int a = 0; a < 3; a++) c->gJ[a] = gb.J[a];
     c->gimg_bytes = (int)(gb.img.size() * sizeof(GridPlane));
     c->grid_cells = (int)gb.cells.size();
@@ -1217,6 +1348,19 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
             if (e == hipSuccess) e = hipStreamSynchronize(c->stream);
             hipFree(d_raw);
             if (e != hipSuccess) return set_err(FMGI_ERR_HIP, "scene setup: %s", hipGetErrorString(e));
+        }
+    }
+    c->nsrcs = num_windows + num_lights; /* (build_compact sizes the staged emitters) */
+    if (try_compact) { /* the compact tables need the device-computed fields: the walls back to the host */
+        std::vector<RectDev> drd((size_t)num_walls);
+        HIPCHK(hipMemcpy(drd.data(), c->d_rects, drd.size() * sizeof(RectDev), hipMemcpyDeviceToHost));
+        if (build_compact(c, drd, fb, gcomp)) {
+            c->compact = true;
+            gb = gcomp;
+            c->gimg_bytes = (int)(gb.img.size() * sizeof(GridPlane));
+            c->grid_cells = (int)gb.cells.size();
+            c->grid_entries = (int)gb.idx.size();
+            c->h_grid = gb;
         }
     }
     hipFree(c->d_fimg);
@@ -1391,6 +1535,7 @@ struct StagePlan {
     int block = 256;
     int bytes = 0;                   /* staged blob = image (16-B aligned) | rects | srcs | cells | overflow */
     int rects_off = -1, srcs_off = -1, cells_off = -1, grecs_off = -1, gidx_off = -1;
+    int rectc_off = -1, class_off = -1, recf_off = -1, cellc_off = -1; /* the compact closed-box tables */
 };
 
 static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs, bool cells, bool grecs, int *roff,
@@ -1436,6 +1581,28 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     const int forced_block = (be && atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) ? atoi(be) : 0;
     p.block = forced_block ? forced_block : 256;
     if (kernel == FMGI_KERNEL_EXACT) return p; /* no LDS image: nothing is staged */
+    if (c->compact && kernel == FMGI_KERNEL_GRID && accum == kAccScatter && c->nsrcs > 0 && !forced_block) {
+        /* the compact closed box: image | emitters | classes | RectC | filter extents | cells, one 1024-lane
+           workgroup per CU (the tables take most of its LDS) */
+        int off = (c->gimg_bytes + 15) & ~15;
+        p.srcs_off = off;
+        off += c->nsrcs * (int)sizeof(SrcDev);
+        p.class_off = off;
+        off += (int)(c->h_classc.size() * sizeof(ClassC));
+        p.rectc_off = off;
+        off += (int)((c->h_rectc.size() * sizeof(RectC) + 15) & ~(size_t)15);
+        p.recf_off = off;
+        off += (int)(c->h_recf.size() * sizeof(float));
+        p.cellc_off = off;
+        off += (int)(c->h_cellc.size() * sizeof(uint32_t));
+        p.bytes = (off + 15) & ~15;
+        p.block = 1024;
+        const int inst = FMGI_KERNEL_GRID | FMGI_KVAR_AXES | FMGI_KVAR_COMPACT;
+        if (fmgi_bake_lds(inst, accum, p.block, p.bytes, nullptr) <= kBakeLdsMax &&
+            fmgi_bake_resident_blocks(inst, accum, trace, p.block, p.bytes) >= 1)
+            return p;
+        p = StagePlan{}; /* (does not launch: the general planning below) */
+    }
     const char *se = getenv("FMGI_SRCS_LDS"), *re = getenv("FMGI_RECTS_LDS");
     const bool srcs = c->nsrcs > 0 && !(se && atoi(se) == 0);
     const int rects_mode = re ? atoi(re) : -1; /* -1 auto */
@@ -1596,6 +1763,7 @@ static int exec_accum(const fmgi_context *c) {
        r05/s5). FMGI_SCATTER=0/1 forces either (experiments, tests). */
     const char *se = getenv("FMGI_SCATTER");
     if (se) return atoi(se) == 1 ? kAccScatter : kAccBucket;
+    if (c->compact) return kAccScatter; /* the compact closed box: every table staged (FMGI_KVAR_COMPACT) */
     const size_t tables = (size_t)c->nrects * sizeof(RectLds) + (c->cells_lds ? (size_t)c->grid_cells * sizeof(GridCell) : 0);
     return tables <= 64 * 1024 ? kAccScatter : kAccBucket;
 }
@@ -1634,9 +1802,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (inst == (FMGI_KERNEL_GRID | FMGI_KVAR_AXES) && sp.rects_off >= 0 && sp.srcs_off >= 0 && sp.cells_off >= 0 &&
         sp.grecs_off >= 0 && !getenv("FMGI_NO_STAGED"))
         inst |= FMGI_KVAR_STAGED;
+    if (inst == (FMGI_KERNEL_GRID | FMGI_KVAR_AXES) && sp.rectc_off >= 0) inst |= FMGI_KVAR_COMPACT;
     /* a closed box built with the coarse LDS grid (5 cells per record) but launched without the cells staged
        reads that coarser grid from L2, slower than the 16-per-record grid it replaced: said once per context */
-    if (c->cells_lds && kernel == FMGI_KERNEL_GRID && sp.cells_off < 0 && !c->warned_cells && !getenv("FMGI_QUIET")) {
+    if (c->cells_lds && kernel == FMGI_KERNEL_GRID && sp.cells_off < 0 && sp.rectc_off < 0 && !c->warned_cells &&
+        !getenv("FMGI_QUIET")) {
         fprintf(stderr, "fmgi: the closed-box grid's cells (%d, built for LDS) are not staged at block %d: "
                         "lookups read L2 (FMGI_CELLS_LDS=0 builds the finer global grid)\n", c->grid_cells, block);
         c->warned_cells = true;
@@ -1696,7 +1866,42 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         for (int k = 0; k < 3; k++) a.fJ[k] = c->fJ[k];
     }
     a.rects_off = a.srcs_off = a.cells_off = a.grecs_off = a.gidx_off = -1;
-    if (sp.rects_off >= 0 || sp.srcs_off >= 0 || sp.cells_off >= 0) { /* the blob: image | rects | srcs | cells */
+    a.rectc_off = a.class_off = a.recf_off = a.cellc_off = -1;
+    a.cdummy = c->nrects;
+    if (sp.rectc_off >= 0) { /* the compact blob: image | srcs | classes | RectC | filter extents | cells */
+        const uint64_t key = (c->scene_gen << 9) | 0x1FFu;
+        if (c->blob_key != key) {
+            if (c->blob_cap < (size_t)sp.bytes) {
+                HIPCHK(hipStreamSynchronize(s)); /* no earlier bake may still stage the old blob */
+                hipFree(c->d_blob);
+                c->d_blob = nullptr;
+                c->blob_cap = 0;
+                HIPCHK(hipMalloc(&c->d_blob, (size_t)sp.bytes));
+                c->blob_cap = (size_t)sp.bytes;
+            }
+            HIPCHK(hipMemsetAsync(c->d_blob, 0, (size_t)sp.bytes, s));
+            if (a.fimg_bytes) HIPCHK(hipMemcpyAsync(c->d_blob, a.fimg, (size_t)a.fimg_bytes, hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->d_blob + sp.srcs_off, c->d_srcs, (size_t)c->nsrcs * sizeof(SrcDev),
+                                  hipMemcpyDeviceToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->d_blob + sp.class_off, c->h_classc.data(), c->h_classc.size() * sizeof(ClassC),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->d_blob + sp.rectc_off, c->h_rectc.data(), c->h_rectc.size() * sizeof(RectC),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->d_blob + sp.recf_off, c->h_recf.data(), c->h_recf.size() * sizeof(float),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(hipMemcpyAsync(c->d_blob + sp.cellc_off, c->h_cellc.data(), c->h_cellc.size() * sizeof(uint32_t),
+                                  hipMemcpyHostToDevice, s));
+            HIPCHK(hipStreamSynchronize(s)); /* (the host tables stay; the copies are done before they could change) */
+            c->blob_key = key;
+        }
+        a.fimg = c->d_blob;
+        a.fimg_bytes = sp.bytes;
+        a.srcs_off = sp.srcs_off;
+        a.rectc_off = sp.rectc_off;
+        a.class_off = sp.class_off;
+        a.recf_off = sp.recf_off;
+        a.cellc_off = sp.cellc_off;
+    } else if (sp.rects_off >= 0 || sp.srcs_off >= 0 || sp.cells_off >= 0) { /* the blob: image | rects | srcs | cells */
         const uint64_t key = (c->scene_gen << 9) | (sp.grecs_off >= 0 ? 0x100u : 0u) |
                              (kernel == FMGI_KERNEL_HYBRID && hybrid_full(c) ? 0x40u : 0u) |
                              ((uint64_t)(kernel & 0xF) << 2) | (sp.rects_off >= 0 ? 2u : 0u) | (sp.srcs_off >= 0 ? 1u : 0u) |

@@ -68,6 +68,35 @@ struct GridCellF {
 };
 static_assert(sizeof(GridCellF) == 48, "GridCellF must be 48 B");
 
+/* The compact closed-box tables (ScanGridT's Compact instance, FMGI_KVAR_COMPACT): closed boxes whose RectLds
+   walls (112 B each) and 32-B grid cells do not fit LDS (BASELINE config 5: 2000 walls) stage instead
+     - RectC: phase 2's per-wall fields, 24 B (2000 walls: 48 KB): pos, length(width), length(height), and
+       meta = texel base (22 bits) | class (10 bits);
+     - ClassC: what walls share, 64 B per distinct bit pattern of {n, width / length(width), height /
+       length(height), sampler basis bu, bv, W, H} (a closed box has a few per plane);
+     - the walls' float filter extents {cu, hwu, cv, hwv} by rect index (16 B; one never-valid dummy after
+       the last wall);
+     - CellC: a grid cell as up to four u16 rect indices (8 B; absent = the dummy), no inline bounds.
+   The host builds RectC / ClassC from the device-computed RectDev and checks that every field round-trips bit
+   for bit (fmgi_api.cpp build_compact); 1 / length, which only the tile index's quotient estimate uses (any
+   value within one ulp gives the same tile, fmgi_core.h trunc_div_inv), is v_rcp_f32 of the length. */
+struct RectC {
+    float px, py, pz, wl;
+    float hl;
+    uint32_t meta; /* texel base | class << 22 */
+};
+static_assert(sizeof(RectC) == 24, "RectC must be 24 B");
+struct __attribute__((aligned(16))) ClassC {
+    float nx, ny, nz, wnx;
+    float wny, wnz, hnx, hny;
+    float hnz, bux, buy, buz;
+    float bvx, bvy, bvz;
+    int32_t WH; /* W | H << 16 */
+};
+static_assert(sizeof(ClassC) == 64, "ClassC must be 64 B");
+constexpr int kCompactBaseBits = 22;
+constexpr int kCompactMaxClasses = 1 << (32 - kCompactBaseBits);
+
 struct BakeArgs {
     const RectDev *rects;
     int nrects;
@@ -116,6 +145,9 @@ struct BakeArgs {
     int fetch_nseg;
     unsigned long long *src_cost; /* non-null: per-source scan totals of the finished items */
     int grid_code_or;     /* ScanHybrid: flag or-ed into the codes of grid records (rect indices)    */
+    /* the compact closed-box instance (FMGI_KVAR_COMPACT): byte offsets in the staged blob of the RectC,
+       ClassC, filter-extent (float4 by rect index) and CellC tables, and the dummy record's index */
+    int rectc_off, class_off, recf_off, cellc_off, cdummy;
     int coop;             /* lanes per work item (1, 2, 4, 8; ScanFast only): small launches split each
                              scan's records over several lanes instead of leaving the GPU mostly idle */
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
@@ -237,6 +269,7 @@ constexpr int kAccSliced = 9; /* the STREAM's unsorted layout alone (BakeArgs::p
 #define FMGI_KVAR_AXES 0x100
 #define FMGI_KVAR_PLAN 0x200 /* FMGI_KERNEL_HYBRID | this: the walls over the floor plan (BakeArgs::plan_off) */
 #define FMGI_KVAR_STAGED 0x400 /* FMGI_KERNEL_GRID | FMGI_KVAR_AXES | this: walls, emitters and cells all in LDS */
+#define FMGI_KVAR_COMPACT 0x800 /* FMGI_KERNEL_GRID | FMGI_KVAR_AXES | this: the compact tables (RectC ...) in LDS */
 hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace, int grid_blocks, int block,
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);

@@ -141,6 +141,32 @@ __device__ __forceinline__ float exact_hit(const BakeArgs &a, int idx, f3 src, f
     return exact_hit_rec(((gptr<RectDev>)a.rects)[idx], idx, src, dir, h);
 }
 
+/* phase 2 on the compact closed-box tables (fmgi_internal.h RectC / ClassC, staged in LDS): the same
+   intersect_exact_uv on the same bit patterns as exact_hit_rec's RectLds / RectDev fields; 1 / length is
+   v_rcp_f32 (tile_uv's quotient estimate needs only one ulp) */
+__device__ __forceinline__ float exact_hit_compact(const BakeArgs &a, const char *lds, int idx, f3 src, f3 dir,
+                                                   HitRec &h) {
+    typedef const __attribute__((address_space(3))) char *lp;
+    const __attribute__((address_space(3))) RectC &r =
+        *(const __attribute__((address_space(3))) RectC *)((lp)lds + a.rectc_off + __umul24((uint32_t)idx, (uint32_t)sizeof(RectC)));
+    const float px = r.px, py = r.py, pz = r.pz, wl = r.wl, hl = r.hl;
+    const uint32_t meta = r.meta;
+    const __attribute__((address_space(3))) ClassC &k =
+        *(const __attribute__((address_space(3))) ClassC *)((lp)lds + a.class_off + ((meta >> kCompactBaseBits) << 6));
+    h.idx = idx;
+    h.nx = k.nx; h.ny = k.ny; h.nz = k.nz;
+    h.wl = wl; h.hl = hl;
+    h.iwl = __builtin_amdgcn_rcpf(wl);
+    h.ihl = __builtin_amdgcn_rcpf(hl);
+    h.base = (int)(meta & ((1u << kCompactBaseBits) - 1));
+    const uint32_t wh = (uint32_t)k.WH;
+    h.W = (int)(wh & 0xFFFFu); h.H = (int)(wh >> 16);
+    h.bux = k.bux; h.buy = k.buy; h.buz = k.buz;
+    h.bvx = k.bvx; h.bvy = k.bvy; h.bvz = k.bvz;
+    return intersect_exact_uv(mkf3(h.nx, h.ny, h.nz), mkf3(px, py, pz), mkf3(k.wnx, k.wny, k.wnz), wl,
+                              mkf3(k.hnx, k.hny, k.hnz), hl, src, dir, h.dx, h.dy);
+}
+
 /* the result of a literal scan (hit, best) as a HitRec (rare paths: ScanExact, fallbacks) */
 __device__ __forceinline__ void finish_hit(const BakeArgs &a, int hit, float best, f3 src, f3 dir, HitRec &h) {
     h = HitRec{}; /* every field is (re)written here, so none of the caller's phase-2 values stays live */
@@ -718,19 +744,43 @@ __device__ __forceinline__ void grid_phase1_sorted(const BakeArgs &a, const char
  * winner's exact fac f, so the separation test `L2 > f (1 + 2^-12)` has the same outcome with or
  * without it (grid_phase1_sorted's argument); equal keys fail that test whatever the order.
  */
-template <int A, bool Staged>
+/* the candidate tests of compact cell ci (CellC: up to four rect indices, absent ones the never-valid dummy):
+   every index's float filter extents {cu, hwu, cv, hwv} from the LDS table by rect index, tested as the float
+   cells' records are (grid_rec); the four reads are issued together, with no branch */
+__device__ __forceinline__ void grid_cell_tests_c(const BakeArgs &a, const char *lds, uint32_t ci, float f, float uh,
+                                                  float vh, float &L1, float &L2, int &code1, unsigned &ntest) {
+    typedef const __attribute__((address_space(3))) char *lp;
+    typedef uint32_t u2v __attribute__((ext_vector_type(2)));
+    typedef float f4v __attribute__((ext_vector_type(4)));
+    const u2v c = *(const __attribute__((address_space(3))) u2v *)((lp)lds + a.cellc_off + 8u * ci);
+    const __attribute__((address_space(3))) f4v *R = (const __attribute__((address_space(3))) f4v *)((lp)lds + a.recf_off);
+    const uint32_t i0 = c.x & 0xFFFFu, i1 = c.x >> 16, i2 = c.y & 0xFFFFu, i3 = c.y >> 16;
+    const f4v r0 = R[i0], r1 = R[i1], r2 = R[i2], r3 = R[i3];
+    const uint32_t D = (uint32_t)uni(a.cdummy);
+    ntest += (unsigned)(i0 != D) + (unsigned)(i1 != D) + (unsigned)(i2 != D) + (unsigned)(i3 != D);
+    grid_rec(f, uh, vh, make_float4(r0.x, r0.y, r0.z, r0.w), (int)i0, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(r1.x, r1.y, r1.z, r1.w), (int)i1, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(r2.x, r2.y, r2.z, r2.w), (int)i2, L1, L2, code1);
+    grid_rec(f, uh, vh, make_float4(r3.x, r3.y, r3.z, r3.w), (int)i3, L1, L2, code1);
+}
+
+template <int A, bool Staged, bool Compact = false>
 __device__ __forceinline__ void grid_axes_visit(const BakeArgs &a, const char *img, f3 s, f3 d, float f, float &L1,
                                                 float &L2, int &code1, unsigned &ntest) {
     constexpr int U = (A == 0) ? 1 : 0;
     constexpr int V = (A == 2) ? 1 : 2;
     const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * A + (comp<A>(d) < 0.0f ? 0 : 64), 16);
     const float uh = fmaf(comp<U>(d), f, comp<U>(s)), vh = fmaf(comp<V>(d), f, comp<V>(s));
+    if (Compact) {
+        grid_cell_tests_c(a, img, grid_cell_idx(p[0], p[1], p[2], uh, vh), f, uh, vh, L1, L2, code1, ntest);
+        return;
+    }
     uint32_t qu, qv;
     const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
     grid_cell_tests<Staged>(a, img, load_cell<Staged>(a, img, ci), f, uh, vh, qu, qv, L1, L2, code1, ntest);
 }
 
-template <bool Staged>
+template <bool Staged, bool Compact = false>
 __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *img, f3 s, f3 d, float &L1,
                                                  float &L2, int &code1, unsigned &ntest) {
     const float fx0 = (*(const float *)(img + (d.x < 0.0f ? 0 : 64)) - s.x) * __builtin_amdgcn_rcpf(d.x);
@@ -751,14 +801,18 @@ __device__ __forceinline__ void grid_phase1_axes(const BakeArgs &a, const char *
         const float du = (m == 0) ? d.y : d.x, dv = mz ? d.y : d.z;
         const float4 *p = (const float4 *)__builtin_assume_aligned(img + 128 * m + (dm < 0.0f ? 0 : 64), 16);
         const float uh = fmaf(du, fm, su), vh = fmaf(dv, fm, sv);
-        uint32_t qu, qv;
-        const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
-        grid_cell_tests<Staged>(a, img, load_cell<Staged>(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
+        if (Compact) {
+            grid_cell_tests_c(a, img, grid_cell_idx(p[0], p[1], p[2], uh, vh), fm, uh, vh, L1, L2, code1, ntest);
+        } else {
+            uint32_t qu, qv;
+            const uint32_t ci = grid_cell(p[0], p[1], p[2], uh, vh, qu, qv);
+            grid_cell_tests<Staged>(a, img, load_cell<Staged>(a, img, ci), fm, uh, vh, qu, qv, L1, L2, code1, ntest);
+        }
     }
     const int m = mz ? 2 : (my ? 1 : 0); /* the others, within the band above the current L1 (1 + 2^-11) */
-    if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0, Staged>(a, img, s, d, fx, L1, L2, code1, ntest);
-    if (m != 1 && fy < INFINITY && fy <= L1 * 1.00048828125f) grid_axes_visit<1, Staged>(a, img, s, d, fy, L1, L2, code1, ntest);
-    if (m != 2 && fz < INFINITY && fz <= L1 * 1.00048828125f) grid_axes_visit<2, Staged>(a, img, s, d, fz, L1, L2, code1, ntest);
+    if (m != 0 && fx < INFINITY && fx <= L1 * 1.00048828125f) grid_axes_visit<0, Staged, Compact>(a, img, s, d, fx, L1, L2, code1, ntest);
+    if (m != 1 && fy < INFINITY && fy <= L1 * 1.00048828125f) grid_axes_visit<1, Staged, Compact>(a, img, s, d, fy, L1, L2, code1, ntest);
+    if (m != 2 && fz < INFINITY && fz <= L1 * 1.00048828125f) grid_axes_visit<2, Staged, Compact>(a, img, s, d, fz, L1, L2, code1, ntest);
 }
 
 /* calls fn(idx) for the rect index of every record that passes grid_axis's candidate test */
@@ -802,10 +856,14 @@ __device__ __forceinline__ void grid_visit(const BakeArgs &a, const char *lds, i
 /* Axes = true: the closed-box specialisation (one plane per axis and class, BakeArgs::grid_axes), whose
    kernel holds grid_phase1_axes alone: the general kernel's register and SGPR budget is set by its layout
    walks, and its spilled SGPRs come back as v_readlane in the box scan too */
-template <bool Axes, bool Staged = false>
+template <bool Axes, bool Staged = false, bool Compact = false>
 struct ScanGridT {
+    static_assert(!Compact || (Axes && Staged), "the compact tables exist for the staged closed-box instance");
     static constexpr bool kLds = true;
     static constexpr bool kCoop = false;
+    /* Compact: one 1024-lane workgroup per CU holds the ~150 KB of compact tables, i.e. 4 waves per SIMD, so the
+       instance takes the registers of 4 */
+    static constexpr int kWaves = Compact ? 4 : 0;
     /* Staged (closed boxes whose walls, emitters, grid cells and the cells' overflow records the plan stages
        in LDS): the global-memory paths of those tables are compiled out, so the bake loop issues no global
        load but its rare fallbacks' and work-item fetches' */
@@ -855,7 +913,7 @@ struct ScanGridT {
         int code1 = -1;
         unsigned ntest = 0;
         if (Axes) {
-            grid_phase1_axes<Staged>(a, lds, src, dir, L1, L2, code1, ntest);
+            grid_phase1_axes<Staged, Compact>(a, lds, src, dir, L1, L2, code1, ntest);
         } else if (a.fJ[0] + a.fJ[1] + a.fJ[2] <= 4) {
             grid_phase1_sorted(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
@@ -887,7 +945,7 @@ struct ScanGridT {
             return;
         }
         const int idx = code1; /* rect index of the phase-1 winner */
-        const float f = exact_hit<Staged>(a, lds, idx, src, dir, h);
+        const float f = Compact ? exact_hit_compact(a, lds, idx, src, dir, h) : exact_hit<Staged>(a, lds, idx, src, dir, h);
         const bool sep = !(f < 0) && L2 > f * 1.000244140625f; /* ScanFast's separation test */
         st.clk.lap(ST_SCAN2);
         if (sep) {
@@ -897,7 +955,7 @@ struct ScanGridT {
         if (f < 0) st.invalid++; else st.ties++;
         float best;
         int r = ordered_exact(a, lds, src, dir, best);
-        if (r == -2) r = ScanExact::literal<false, Staged>(a, lds, src, dir, best, st);
+        if (r == -2) r = ScanExact::literal<false, Staged && !Compact>(a, lds, src, dir, best, st); /* (compact: global) */
         finish_hit(a, r, best, src, dir, h);
         st.clk.lap(ST_FALLBACK);
     }
@@ -906,6 +964,7 @@ struct ScanGridT {
 using ScanGrid = ScanGridT<false>;
 using ScanGridAxes = ScanGridT<true>;
 using ScanGridAxesStaged = ScanGridT<true, true>;
+using ScanGridAxesCompact = ScanGridT<true, true, true>;
 
 /*
  * ScanHybrid's wall pass over the floor plan (Plan = true; tables: fmgi_api.cpp build_plan, which holds
@@ -2002,8 +2061,18 @@ __device__ __forceinline__ uint32_t lcg2(uint32_t s) {
 #define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(FMGI_WAVES_PER_EU)))
 #else /* ScanGrid: 4 waves/SIMD (108 VGPRs, no spills): with the walls staged, LDS holds a CU to 16 waves anyway;
          AccLines leaves the LDS for 6 (768-lane workgroups, two per CU) and asks for the registers of 6 */
-#define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(acc_min_waves<Acc>() > Scan::kMinWaves ? acc_min_waves<Acc>() : Scan::kMinWaves)))
+#define FMGI_BAKE_ATTR __attribute__((amdgpu_waves_per_eu(ScanWaves<Scan>::value ? ScanWaves<Scan>::value \
+    : (acc_min_waves<Acc>() > Scan::kMinWaves ? acc_min_waves<Acc>() : Scan::kMinWaves))))
 #endif
+/* a scan instance whose occupancy is fixed by its LDS tables (ScanGridT::kWaves), else 0 */
+template <class Scan, class = void>
+struct ScanWaves {
+    static constexpr int value = 0;
+};
+template <class Scan>
+struct ScanWaves<Scan, decltype((void)Scan::kWaves)> {
+    static constexpr int value = Scan::kWaves;
+};
 template <class Acc>
 constexpr int acc_min_waves() { return 1; }
 template <>
@@ -2420,6 +2489,8 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
                : accum == kAccDense ? kernel_ptr<ScanFastCoop, AccDense>(false)
                : accum == kAccSliced ? kernel_ptr<ScanFastCoop, AccSliced>(false)
                                     : kernel_ptr<ScanFastCoop, AccStream>(false);
+    if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_COMPACT)) /* the lane-by-lane stores only (bake_common) */
+        return accum == kAccScatter ? kernel_ptr<ScanGridAxesCompact, AccScatter>(trace) : nullptr;
     if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) return kernel_acc<ScanGridAxesStaged>(accum, trace);
     if (kernel == (2 | FMGI_KVAR_AXES)) return kernel_acc<ScanGridAxes>(accum, trace);
     if (kernel == (4 | FMGI_KVAR_PLAN)) return kernel_acc<ScanHybridPlan>(accum, trace);
@@ -2496,6 +2567,9 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
         launch_acc<ScanHybrid>(a, accum, trace, grid, blk, lds, s);
+    } else if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_COMPACT)) { /* closed box, the compact tables in LDS */
+        if (accum != kAccScatter) return hipErrorInvalidValue;
+        launch3<ScanGridAxesCompact, AccScatter>(a, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) { /* closed box, every table in LDS */
         launch_acc<ScanGridAxesStaged>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES)) { /* FMGI_KERNEL_GRID, closed box */

@@ -208,3 +208,20 @@ def test_grid_is_small_and_selective(box200, box2000):
         ent = sum(int(c["count"].sum()) for _, c in planes)
         assert tot <= 16 * len(sc.walls) + 16 * 6
         assert ent / tot < 2.0, ent / tot
+
+
+@pytest.mark.parametrize("cpr", [4, 3, 2])
+def test_compact_grids_cover_and_hold_four_records(cpr, box2000, monkeypatch):
+    """The grids the compact closed-box tables index (fmgi_api.cpp build_compact, BASELINE config 5: 4, 3 or 2
+    cells per record, each cell's records as up to four u16 indices): the coverage property of every grid, and
+    no box2000 cell of more than four records, so every cell fits its CellC."""
+    monkeypatch.setenv("FMGI_GRID_CPR", str(cpr))
+    t = _tables(box2000)
+    rng = np.random.default_rng(11 + cpr)
+    n = 0
+    planes = _planes(t)
+    assert len(planes) == 6
+    for p, cells in planes:
+        n += _check_plane(t, p, cells, rng)
+        assert int(cells["count"].max()) <= 4
+    assert n == len(box2000.walls) < 0xFFFF

@@ -2,7 +2,7 @@
 # One gpurun session. Steps (FMGI_STEPS, space separated):
 #   tests            pytest -m gpu
 #   smoke            __graft_entry__.smoke()
-#   tests_k          pytest -m gpu $TESTS_ARGS (e.g. '-k radiosity')
+#   tests_k          pytest -m gpu $TESTS_ARGS, with -k "$TESTS_K" when set
 #   rad / radprof    tools/bench_rad.py $RAD_ARGS (plain / under rocprofv3 --kernel-trace --stats)
 #   ref              reference-kernel pin (tests/golden/make_ref_fixtures.py)
 #   tol              whole-launch reference sums, strict and relaxed (tests/golden/make_tolerance_fixtures.py)
@@ -43,7 +43,11 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
   case $s in
     tests) step tests 1100 python -u -m pytest tests -m gpu -v -x -p no:cacheprovider --timeout 900 --timeout-method thread ;;
     smoke) step smoke 300 python -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" ;;
-    tests_k) step tests_k 900 python -u -m pytest -m gpu -v -x -p no:cacheprovider --timeout 120 --timeout-method thread ${TESTS_ARGS:-tests} ;;
+    tests_k) if [ -n "${TESTS_K:-}" ]; then
+               step tests_k 900 python -u -m pytest -m gpu -v -x -p no:cacheprovider --timeout 300 --timeout-method thread -k "$TESTS_K" ${TESTS_ARGS:-tests}
+             else
+               step tests_k 900 python -u -m pytest -m gpu -v -x -p no:cacheprovider --timeout 300 --timeout-method thread ${TESTS_ARGS:-tests}
+             fi ;;
     rad)   step rad 900 python tools/bench_rad.py ${RAD_ARGS:-} ;;
     radprof) step radprof 900 rocprofv3 --kernel-trace --stats -d "$OUT/radprof" -o run --output-format csv -- python tools/bench_rad.py --reps 1 --no-cpu-baseline ${RAD_ARGS:-} ;;
     ref)   step ref 600 python tests/golden/make_ref_fixtures.py "$OUT" ;;

@@ -1,0 +1,211 @@
+#!/usr/bin/env python
+"""Per-stage instruction counts of one k_bake instance's bake loop, from its gfx950 ISA.
+
+Every instruction of the kernel is attributed to the bake stage of the source it was generated from, using
+the inlining chain llvm-symbolizer reports for its address in a debug build of the same kernel source
+(hipcc -g only adds debug sections; the tool checks that the instance's VGPR count equals the product
+build's). The loop is the kernel's outermost backward branch. Basic blocks whose instructions mostly come
+from rare paths (near-tie fallbacks, pool-block allocation, work-item fetch and per-item bookkeeping) are
+counted apart: a wave executes every other block of the loop on almost every iteration, since a branch taken
+by any of its 64 lanes is issued for the whole wave (the deposit, the diffuse/mirror choice and the floor
+tint are lane-divergent, not rare). The non-rare static count is therefore the per-iteration dynamic count
+of a wave, to compare with SQ_INSTS_VALU per wave-scan.
+
+  python tools/isa_stages.py [--kernel SUBSTRING] [--json OUT]
+"""
+import argparse
+import collections
+import json
+import os
+import re
+import subprocess
+import sys
+
+REPO = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PKG = os.path.join(REPO, "flatmatch-global-illumination_amd")
+LLVM = "/opt/rocm/lib/llvm/bin"
+
+# innermost-first: the first function of an instruction's inlining chain found here names its stage
+STAGE_OF_FUNC = [
+    ("fmgi_sincosf", "sampler: OCML sin/cos"),
+    ("sqrt_cr", "sampler: sqrt_cr (2)"),
+    ("rng_next", "RNG draws"),
+    ("lcg2", "RNG draws"),
+    ("sample_dir", "sampler: basis combination"),
+    ("ordered_exact", "fallback (rare)"),
+    ("literal", "fallback (rare)"),
+    ("finish_hit", "fallback (rare)"),
+    ("grid_visit", "fallback (rare)"),
+    ("coop_merge", "fallback (rare)"),
+    ("alloc", "pool block allocation (rare)"),
+    ("locate_item", "work-item fetch (rare)"),
+    ("intersect_exact_uv", "phase 2: exact intersects()"),
+    ("exact_hit_rec", "phase 2: record fields"),
+    ("exact_hit_compact", "phase 2: record fields"),
+    ("exact_hit", "phase 2: record fields"),
+    ("grid_cell_tests_c", "phase 1: cell record tests"),
+    ("grid_cell_tests", "phase 1: cell record tests"),
+    ("grid_recq", "phase 1: cell record tests"),
+    ("grid_rec", "phase 1: cell record tests"),
+    ("grid_qpass", "phase 1: cell record tests"),
+    ("load_cell", "phase 1: cell lookup"),
+    ("grid_cell_idx", "phase 1: cell lookup"),
+    ("grid_cell", "phase 1: cell lookup"),
+    ("grid_axes_visit", "phase 1: other planes in the band"),
+    ("grid_phase1_axes", "phase 1: nearest plane"),
+    ("trunc_div_inv", "tile index"),
+    ("tile_uv", "tile index"),
+    ("append", "deposit code: tile word + store"),
+    ("load_src", "emission: emitter fields"),
+    ("src_fields", "emission: emitter fields"),
+]
+RARE = {"fallback (rare)", "pool block allocation (rare)", "work-item fetch (rare)"}
+
+
+def k_bake_line_stage(src_lines, line):
+    """a stage for code that is k_bake's own (not inlined from a helper), from the comment markers in its body"""
+    marks = [("---- stage 1", "emission / new photon"), ("---- stage 2", "scan (k_bake glue)"),
+             ("---- stage 3", "hit: position, roulette, colour, code"), ("Acc::append(a, ws", "deposit code: tile word + store"),
+             ("#ifdef FMGI_CLOCK_STAMP /* sum over waves", "after the loop")]
+    stage = "loop control"
+    for i, l in enumerate(src_lines[:line], 1):
+        for m, st in marks:
+            if m in l:
+                stage = st
+    return stage
+
+
+def classify(chain, src_lines):
+    for fn, _, _ in chain:
+        for key, st in STAGE_OF_FUNC:
+            if re.search(r"(^|::|\b)" + re.escape(key) + r"(<|\(|$)", fn):
+                return st
+    fn, path, line = chain[-1] if chain else ("?", "", 0)
+    if "k_bake" in fn and path.endswith("fmgi_kernels.hip"):
+        return k_bake_line_stage(src_lines, line)
+    return "other: " + fn.split("(")[0][-40:]
+
+
+def kind(mn):
+    if mn.startswith("v_"):
+        return "VALU"
+    if mn.startswith("ds_"):
+        return "LDS"
+    if mn.startswith(("global_", "buffer_", "flat_", "scratch_")):
+        return "VMEM"
+    if mn.startswith(("s_load", "s_buffer", "s_store", "s_memtime", "s_memrealtime")):
+        return "SMEM"
+    if mn.startswith(("s_cbranch", "s_branch", "s_setpc", "s_swappc")):
+        return "BRANCH"
+    if mn.startswith("s_waitcnt") or mn.startswith(("s_nop", "s_barrier", "s_sleep", "s_sched", "s_setprio")):
+        return "WAIT/NOP"
+    if mn.startswith("s_"):
+        return "SALU"
+    return "OTHER"
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--kernel", default="k_bakeINS_9ScanGridTILb1ELb1ELb0EEENS_10AccScatterELb0E")
+    ap.add_argument("--obj", default="/tmp/fmgi_kernels_dbg.o")
+    ap.add_argument("--rebuild", action="store_true")
+    ap.add_argument("--json")
+    a = ap.parse_args()
+    if a.rebuild or not os.path.exists(a.obj):
+        bundle = a.obj + ".bundle"
+        subprocess.run(["/opt/rocm/bin/hipcc", "-O3", "-std=c++17", "-ffp-contract=off", "-fno-fast-math",
+                        "--offload-arch=gfx950", "-munsafe-fp-atomics", "-fno-slp-vectorize", "-I" + os.path.join(PKG, "csrc"),
+                        "-I" + os.path.join(REPO, "include"), "--offload-device-only", "-c", "-g", "-o", bundle,
+                        os.path.join(PKG, "csrc", "fmgi_kernels.hip")], check=True, stderr=subprocess.DEVNULL)
+        subprocess.run([f"{LLVM}/clang-offload-bundler", "--unbundle", f"--input={bundle}", f"--output={a.obj}",
+                        "--type=o", "--targets=hipv4-amdgcn-amd-amdhsa--gfx950"], check=True)
+    syms = subprocess.run([f"{LLVM}/llvm-objdump", "-t", a.obj], capture_output=True, text=True, check=True).stdout
+    fn = [l for l in syms.splitlines() if a.kernel in l and " F .text" in l]
+    if len(fn) != 1:
+        raise SystemExit(f"{len(fn)} functions match {a.kernel!r}")
+    parts = fn[0].split()
+    start, size, name = int(parts[0], 16), int(parts[4], 16), parts[-1]
+    vgpr = [l for l in syms.splitlines() if name + ".num_vgpr" in l]
+    dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", f"--start-address={start}",
+                          f"--stop-address={start + size}", a.obj], capture_output=True, text=True, check=True).stdout
+    insts = []  # (addr, mnemonic, operands)
+    for l in dis.splitlines():
+        m = re.match(r"\s+(\S+)\s*(.*?)\s*//\s*([0-9A-F]+):", l)
+        if m:
+            insts.append((int(m.group(3), 16), m.group(1), m.group(2)))
+    addrs = "\n".join(hex(x[0]) for x in insts) + "\n"
+    out = subprocess.run([f"{LLVM}/llvm-symbolizer", f"--obj={a.obj}", "--inlining", "--functions=short"],
+                         input=addrs, capture_output=True, text=True, check=True).stdout
+    chains = [[]]
+    lines = out.split("\n")
+    i = 0
+    while i < len(lines) and len(chains) <= len(insts):
+        if lines[i] == "":
+            chains.append([])
+            i += 1
+            continue
+        f = lines[i]
+        loc = lines[i + 1] if i + 1 < len(lines) else ""
+        mm = re.match(r"(.*):(\d+):\d+$", loc)
+        chains[-1].append((f, mm.group(1) if mm else loc, int(mm.group(2)) if mm else 0))
+        i += 2
+    chains = [c for c in chains if c][: len(insts)]
+    src = open(os.path.join(PKG, "csrc", "fmgi_kernels.hip")).read().splitlines()
+    # basic blocks: targets of branches and the instruction after each branch start one
+    tgt = set()
+    back = []
+    for k, (ad, mn, ops) in enumerate(insts):
+        if mn.startswith(("s_cbranch", "s_branch")):
+            m = re.search(r"<[^>]*\+0x([0-9a-f]+)>", ops) or re.search(r"0x([0-9a-f]+)", ops)
+            # llvm-objdump prints the target as an absolute address in a comment-less operand
+            t = None
+            mt = re.search(r"(\d+)$", ops.strip())
+            if mt:
+                t = ad + 4 + 4 * int(mt.group(1)) if False else None
+            tgt.add(k + 1)
+    # targets: objdump prints "s_branch 1234" (a signed dword offset): recompute
+    for k, (ad, mn, ops) in enumerate(insts):
+        if mn.startswith(("s_cbranch", "s_branch")):
+            mt = re.search(r"(-?\d+)\s*$", ops.strip())
+            if not mt:
+                continue
+            t_addr = ad + 4 + 4 * int(mt.group(1))
+            j = next((q for q, x in enumerate(insts) if x[0] == t_addr), None)
+            if j is not None:
+                tgt.add(j)
+                if j <= k:
+                    back.append((j, k))
+    if not back:
+        raise SystemExit("no loop found")
+    lo, hi = max(back, key=lambda x: x[1] - x[0])
+    starts = sorted(x for x in tgt | {lo, hi + 1} if lo <= x <= hi + 1)
+    blocks = [(starts[q], starts[q + 1]) for q in range(len(starts) - 1) if starts[q] < starts[q + 1]]
+    per = collections.defaultdict(lambda: collections.Counter())
+    rare = collections.defaultdict(lambda: collections.Counter())
+    for b0, b1 in blocks:
+        st = [classify(chains[q], src) for q in range(b0, b1)]
+        nrare = sum(s in RARE for s in st)
+        is_rare = nrare * 2 > (b1 - b0)
+        for q in range(b0, b1):
+            (rare if is_rare else per)[st[q - b0]][kind(insts[q][1])] += 1
+    kinds = ["VALU", "SALU", "LDS", "VMEM", "SMEM", "BRANCH", "WAIT/NOP"]
+    tot = collections.Counter()
+    for c in per.values():
+        tot.update(c)
+    res = {"kernel": name, "num_vgpr": int(vgpr[0].split()[0], 16) if vgpr else None,
+           "loop_insts": hi - lo + 1, "blocks": len(blocks),
+           "per_iteration": {s: dict(c) for s, c in sorted(per.items(), key=lambda x: -x[1]["VALU"])},
+           "per_iteration_total": dict(tot),
+           "rare_blocks": {s: dict(c) for s, c in rare.items()}}
+    print(f"{name}\n  VGPRs {res['num_vgpr']}; loop of {res['loop_insts']} instructions in {len(blocks)} blocks")
+    print(f"  {'stage (blocks a wave issues on almost every iteration)':58s}" + "".join(f"{k:>9s}" for k in kinds))
+    for s, c in sorted(per.items(), key=lambda x: -x[1]["VALU"]):
+        print(f"  {s:58s}" + "".join(f"{c.get(k, 0):9d}" for k in kinds))
+    print(f"  {'total':58s}" + "".join(f"{tot.get(k, 0):9d}" for k in kinds))
+    print("  rare blocks: " + ", ".join(f"{s} {c.get('VALU', 0)} VALU" for s, c in rare.items()))
+    if a.json:
+        json.dump(res, open(a.json, "w"), indent=1)
+
+
+if __name__ == "__main__":
+    main()
