@@ -496,6 +496,7 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
     }
 }
 
+#if FMGI_EXPERIMENTS
 /* The binning pass of the dense stream (kAccDense, BakeArgs::presort == 3): the bake wrote one code or
    sentinel per lane and iteration, in no order; k_bin groups them into the bucket layout k_bucket_fold reads
    (pool blocks of FMGI_BUCKET_BLOCK codes, each holding one fold tile's codes, its tile and length recorded).
@@ -651,12 +652,15 @@ __global__ __launch_bounds__(kBinThreads, 8) void k_bin(const uint32_t *__restri
     }
 }
 
+#endif // FMGI_EXPERIMENTS
+
 } // namespace
 
 /* fold tiles per bucket tile for a bucket layout of 2^tb-texel tiles: FMGI_FOLD_SPLIT (1, 2 or 4) if set and
    an instance exists, else 1 */
 int fmgi_fold_split(int tb) {
-    const char *e = getenv("FMGI_FOLD_SPLIT");
+    if (!FMGI_EXPERIMENTS) return 1;
+    const char *e = fmgi_exp_env("FMGI_FOLD_SPLIT");
     const int env = e ? atoi(e) : 0;
     const int want = env > 0 ? env : FMGI_FOLD_SPLIT_DEFAULT;
     if (tb == 12 && (want == 1 || want == 2)) return want;
@@ -672,6 +676,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
     const int split = sb.presort >= 2 ? fmgi_fold_split(tb) : 1;
     const int fb = tb - (split == 4 ? 2 : split == 2 ? 1 : 0);
     const size_t plds = (size_t)3 * ((size_t)1 << fb) * 8 + (size_t)FMGI_COLOUR_STATES * 16;
+#if FMGI_EXPERIMENTS
     if (sb.presort == 3) { /* the dense stream: binned into the pool, then folded as the bucket layout */
         hipError_t e = fmgi_set_lds_attr_once<6>((const void *)k_bin, kBinBatch * 4);
         if (e != hipSuccess) return e;
@@ -681,6 +686,9 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
         e = hipGetLastError();
         if (e != hipSuccess) return e;
     }
+#else
+    if (sb.presort == 3 || sb.presort == 1) return hipErrorInvalidValue; /* (experiment builds' layouts) */
+#endif
     if (sb.presort >= 2) {
         /* the blocks listed by tile (counts, then each workgroup's range in its tiles' parts), then the sums */
         const unsigned lg = (unsigned)((sb.pool_blocks + (uint64_t)kListThreads * kListPerThread - 1) /
@@ -691,45 +699,38 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                            P, sb.tile_blocks);
         hipLaunchKernelGGL(k_bucket_list, dim3(lg), dim3(kListThreads), 0, s, sb.block_tile, sb.cursor, sb.pool_blocks, P,
                            sb.tile_blocks, sb.tile_blocks + FMGI_PRESORT_MAX_TILES + 1, sb.block_list);
-        const char *xe = getenv("FMGI_EXP_FOLD");
-        const int exp = xe ? atoi(xe) : 0;
         typedef void (*FoldFn)(const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, int, int, int,
                                const uint4 *, unsigned long long *, int);
-        static const FoldFn folds[] = {k_bucket_fold<0>, k_bucket_fold<1>, k_bucket_fold<2>, k_bucket_fold<3>,
-                                       k_bucket_fold<4>};
         FoldFn fn = nullptr;
-        if (tb == FMGI_TILE_BITS && split == 1) fn = folds[exp >= 0 && exp <= 4 ? exp : 0];
-        else if (tb == 12 && split == 1) fn = k_bucket_fold<0, 12, 1>;
-        else if (tb == 12 && split == 2) fn = k_bucket_fold<0, 11, 2>;
-        else if (tb == 13 && split == 2) fn = k_bucket_fold<0, 12, 2>;
-        else if (tb == 13 && split == 4) fn = k_bucket_fold<0, 11, 4>;
-        else return hipErrorInvalidValue; /* no instance for this tile width and split */
-        {
-            const char *ce = getenv("FMGI_FOLD_CARRY"); /* experiments: 1 = G/B, 2 = R/G/B carry words */
-            const int carry = ce ? atoi(ce) : 0;
+        if (split == 1 && tb == FMGI_TILE_BITS) fn = k_bucket_fold<0>;
+        else if (split == 1 && tb == 12) fn = k_bucket_fold<0, 12, 1>;
+#if FMGI_EXPERIMENTS
+        {   /* FMGI_EXP_FOLD (profiling variants), FMGI_FOLD_SPLIT (split folds), FMGI_FOLD_CARRY (carry words) */
+            const char *xe = fmgi_exp_env("FMGI_EXP_FOLD"), *ce = fmgi_exp_env("FMGI_FOLD_CARRY");
+            const int exp = xe ? atoi(xe) : 0, carry = ce ? atoi(ce) : 0;
+            static const FoldFn folds[] = {k_bucket_fold<0>, k_bucket_fold<1>, k_bucket_fold<2>, k_bucket_fold<3>,
+                                           k_bucket_fold<4>};
+            if (split == 1 && tb == FMGI_TILE_BITS && exp >= 1 && exp <= 4) fn = folds[exp];
+            if (tb == 12 && split == 2) fn = k_bucket_fold<0, 11, 2>;
+            if (tb == 13 && split == 2) fn = k_bucket_fold<0, 12, 2>;
+            if (tb == 13 && split == 4) fn = k_bucket_fold<0, 11, 4>;
             const bool plain = split == 1 && (tb == 12 || exp == 0);
             if (plain && carry == 1) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 1> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1>;
             if (plain && carry == 2) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 2> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
         }
-        e = fn == folds[0]                            ? fmgi_set_lds_attr_once<3>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, 12, 1> ? fmgi_set_lds_attr_once<7>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, 11, 2> ? fmgi_set_lds_attr_once<8>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, 12, 2> ? fmgi_set_lds_attr_once<9>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, 11, 4> ? fmgi_set_lds_attr_once<10>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, 12, 1, 1> ? fmgi_set_lds_attr_once<11>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, 12, 1, 2> ? fmgi_set_lds_attr_once<12>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1> ? fmgi_set_lds_attr_once<13>((const void *)fn, (int)plds)
-            : fn == (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2> ? fmgi_set_lds_attr_once<14>((const void *)fn, (int)plds)
-                                                    : hipFuncSetAttribute((const void *)fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)plds);
+#endif
+        if (!fn) return hipErrorInvalidValue; /* no instance for this tile width and split */
+        e = fmgi_set_lds_attr_fn((const void *)fn, (int)plds);
         if (e != hipSuccess) return e;
         const int G = (sb.groups + 7) & ~7;
-        const char *be = getenv("FMGI_FOLD_BALANCE"); /* experiments: 0 = equal groups per tile */
+        const char *be = fmgi_exp_env("FMGI_FOLD_BALANCE"); /* experiments: 0 = equal groups per tile */
         const int balanced = be ? atoi(be) != 0 : 1;
         const dim3 grid((unsigned)(P * G * split)), blk(sb.block > 0 ? sb.block : 1024);
         hipLaunchKernelGGL(fn, grid, blk, plds, s, sb.stream, sb.block_list, sb.block_len, sb.tile_blocks, P, G,
                            balanced, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
+#if FMGI_EXPERIMENTS
     if (sb.presort) {
         hipError_t e = fmgi_set_lds_attr_once<2>((const void *)k_tile_runs_pre<FMGI_RING_CODES, 16>, (int)plds);
         if (e != hipSuccess) return e;
@@ -738,6 +739,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                            sb.stream, sb.toff, sb.cursor, sb.cap, P, G, (const uint4 *)sb.colpack, lm, num_texels);
         return hipGetLastError();
     }
+#endif
     const size_t lds = (size_t)3 * kTileTexels * 8 + (size_t)FMGI_COLOUR_STATES * 16; /* 64 KiB: two workgroups per CU */
     const int G = (sb.groups + 7) & ~7; /* a multiple of 8 for the XCD-aware order */
     /* a slice's run of one tile averages slice / P codes: past 128 tiles the slices are 32768 codes (runs
@@ -745,7 +747,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
        stays HBM-bound) and a wave packs 16 slices' runs onto its lanes (k_tile_runs_pre over slices);
        below, 8192-code slices and one run at a time (FMGI_PACKED_RUNS=0/1 forces either, experiments) */
     bool packed = P > 128;
-    if (const char *pe = getenv("FMGI_PACKED_RUNS")) packed = atoi(pe) != 0;
+    if (const char *pe = fmgi_exp_env("FMGI_PACKED_RUNS")) packed = atoi(pe) != 0;
     if (packed) {
         constexpr int kBig = FMGI_STREAM_SLICE_BIG;
         const uint64_t nslices = (sb.cap + kBig - 1) / kBig;

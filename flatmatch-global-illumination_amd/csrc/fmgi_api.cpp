@@ -311,9 +311,10 @@ static uint32_t grid_bounds(float c, float hw, float o, float inv, int cell) {
     return grid_q(a, o, inv, cell) | (grid_q(b, o, inv, cell) << 16);
 }
 
-/* cells per record the grid's cost model may spend (FMGI_GRID_CPR, experiments; 0 if unset) */
+/* cells per record the grid's cost model may spend when forced (FMGI_GRID_CPR, experiment builds; 0 if unset);
+   fmgi_set_grid_cells_per_record sets it per context (tests of the grids the product builds) */
 static int grid_cpr_env() {
-    const char *ce = getenv("FMGI_GRID_CPR");
+    const char *ce = fmgi_exp_env("FMGI_GRID_CPR");
     return ce && atoi(ce) >= 1 && atoi(ce) <= 64 ? atoi(ce) : 0;
 }
 
@@ -591,7 +592,7 @@ PlanBuild build_plan(const FilterBuild &fb, const fmgi_rect *srcs, int ns) {
     };
     const double big = std::max(ex, ey);
     int m_lo = 4, m_hi = 64;
-    if (const char *pe = getenv("FMGI_PLAN_CELLS"))
+    if (const char *pe = fmgi_exp_env("FMGI_PLAN_CELLS"))
         if (atoi(pe) >= 1 && atoi(pe) <= 256) m_lo = m_hi = atoi(pe);
     double best = 1e300;
     for (int m = m_lo; m <= m_hi; m++) {
@@ -739,12 +740,18 @@ struct fmgi_context {
     bool warned_cells = false;        /* the coarse LDS grid was launched unstaged (said once)          */
     /* the compact closed-box tables (fmgi_internal.h RectC ...; build_compact): set when a closed box's
        RectLds walls and 32-B cells do not fit LDS but these do; the grid is then the one they index */
+    int grid_cpr = 0; /* fmgi_set_grid_cells_per_record: the grid's cells per record (0: the product's choice) */
+    /* fmgi_set_option: the tests' handles on product paths a given scene would not take (include/flatmatch_gi.h) */
+    int64_t opt[FMGI_OPT_COUNT] = {0, 0, 0, -1, -1, -1, 0, 0};
     bool compact = false;
     std::vector<RectC> h_rectc;
     std::vector<ClassC> h_classc;
     std::vector<float> h_recf;     /* {cu, hwu, cv, hwv} by rect index, then the dummy */
     std::vector<uint32_t> h_cellc; /* two u32 per cell: idx0 | idx1 << 16, idx2 | idx3 << 16 */
 };
+
+/* the closed-box (one plane per axis and class) instances off: FMGI_OPT_NO_AXES (tests; at fmgi_set_scene) */
+static bool no_axes(const fmgi_context *c) { return c->opt[FMGI_OPT_NO_AXES] != 0 || fmgi_exp_env("FMGI_NO_AXES"); }
 
 FMGI_API const char *fmgi_version(void) { return "fmgi 0.1 (gfx950)"; }
 FMGI_API const char *fmgi_last_error(void) { return g_err.c_str(); }
@@ -941,7 +948,8 @@ static int tiles_of(const fmgi_context *c, int bits) { return (c->num_texels + (
    profiles/r05/s16). So: wide from 3e6 work items (3e8 photons) per chunk. FMGI_WIDE_TILES=0/1 forces. */
 static int tile_bits(const fmgi_context *c, int mode, uint64_t items) {
     if (mode < kStreamBuckets) return FMGI_TILE_BITS;
-    if (const char *we = getenv("FMGI_WIDE_TILES")) { /* 0 / 1 (= 12) or the tile bits, 11-13 */
+    if (c->opt[FMGI_OPT_WIDE_TILES] >= 0) return c->opt[FMGI_OPT_WIDE_TILES] ? FMGI_WIDE_TILE_BITS : FMGI_TILE_BITS;
+    if (const char *we = fmgi_exp_env("FMGI_WIDE_TILES")) { /* experiments: 0 / 1 (= 12) or the tile bits, 11-13 */
         const int v = atoi(we);
         return v == 1 ? FMGI_WIDE_TILE_BITS : (v >= 11 && v <= 13 ? v : FMGI_TILE_BITS);
     }
@@ -990,10 +998,10 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     uint64_t entries = 0;
     if (mode >= kStreamBuckets) {
         sb.pool_blocks = bucket_pool_blocks(cap, P, grid, block);
-        /* FMGI_POOL_LIMIT=n (tests): at most n pool blocks, so the bake runs out of them and takes the
+        /* FMGI_OPT_POOL_LIMIT = n (tests): at most n pool blocks, so the bake runs out of them and takes the
            exact atomic fallback (bucket_atomic) for the rest of its codes */
-        if (const char *pl = getenv("FMGI_POOL_LIMIT"))
-            if (atoll(pl) > 0) sb.pool_blocks = std::min<uint64_t>(sb.pool_blocks, (uint64_t)atoll(pl));
+        if (c->opt[FMGI_OPT_POOL_LIMIT] > 0)
+            sb.pool_blocks = std::min<uint64_t>(sb.pool_blocks, (uint64_t)c->opt[FMGI_OPT_POOL_LIMIT]);
         entries = 3 * sb.pool_blocks * 2; /* three u32 arrays, in u16 units */
         if (!sb.tile_blocks) HIPCHK(hipMalloc(&sb.tile_blocks, 2 * (FMGI_PRESORT_MAX_TILES + 1) * sizeof(uint32_t)));
     } else {
@@ -1020,7 +1028,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
     {
         const int ncu = std::max(1, c->num_cus);
         const int Pf = tiles_of(c, mode >= kStreamBuckets ? tbits : FMGI_TILE_BITS); /* the fold's tiles */
-        const char *ge = getenv("FMGI_FOLD_GROUPS"); /* experiments */
+        const char *ge = fmgi_exp_env("FMGI_FOLD_GROUPS"); /* experiments */
         /* bucketed: ~36 rounds (box200, 46 tiles: fold 11.22 / 10.86 / 10.92 / 11.19 / 12.70 ms at 96 / 200 /
            300 / 800 / 1600 groups, profiles/r03/s21-s22: finer shares of the largest tiles against the
            per-workgroup set-up and flush) */
@@ -1046,7 +1054,7 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
                 sb.groups = (int)std::min<uint64_t>((uint64_t)sb.groups,
                                                     std::max<uint64_t>(8, cap / ((uint64_t)P * FMGI_STREAM_SLICE_BIG)));
         }
-        const char *be = getenv("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
+        const char *be = fmgi_exp_env("FMGI_FOLD_BLOCK"); /* experiments: 256, 512 or 1024 */
         sb.block = (be && (atoi(be) == 256 || atoi(be) == 512 || atoi(be) == 1024)) ? atoi(be) : 1024;
     }
     return FMGI_OK;
@@ -1083,7 +1091,7 @@ FMGI_API int fmgi_get_accumulation(fmgi_context *c) { return c ? c->accum : set_
 /* workgroup size of the bake (FMGI_BLOCK: experiments, 64..1024 lanes) */
 static int bake_block() {
     int block = 256;
-    if (const char *be = getenv("FMGI_BLOCK"))
+    if (const char *be = fmgi_exp_env("FMGI_BLOCK"))
         if (atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) block = atoi(be);
     return block;
 }
@@ -1099,7 +1107,7 @@ static const size_t kBakeLdsMax = 160 * 1024;
 /* whether a hybrid bake reads the full image (the floor-plan walk, FMGI_PLAN=1, or the one-record wall loop
    of FMGI_FILTER_PK=0 builds) rather than the default one (plane image + wall pairs only) */
 static bool hybrid_full(const fmgi_context *c) {
-    const char *pe = getenv("FMGI_PLAN"), *fe = getenv("FMGI_HYB_FULL"); /* FMGI_HYB_FULL=1: A/B of the image */
+    const char *pe = fmgi_exp_env("FMGI_PLAN"), *fe = fmgi_exp_env("FMGI_HYB_FULL"); /* FMGI_HYB_FULL=1: A/B of the image */
     return !fmgi_kernels_filter_pk() || (c->plan_off >= 0 && pe && atoi(pe) == 1) || (fe && atoi(fe) == 1);
 }
 
@@ -1245,7 +1253,8 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->h_fimg = fb.img;
     c->ngeneral = (int)fb.general.size();
     c->margin = fb.margin;
-    GridBuild gb = build_grid(fb, grid_cpr_env() ? grid_cpr_env() : 16);
+    const int cpr_forced = c->grid_cpr > 0 ? c->grid_cpr : grid_cpr_env();
+    GridBuild gb = build_grid(fb, cpr_forced ? cpr_forced : 16);
     /* closed boxes (one plane per class on each axis, the closed-box instance): the coarsest grid of 5 or 4
        cells per record whose cells fit in 32 KB, staged in LDS beside the rings (plan_stage) when that
        keeps the wave count: every cell lookup an LDS read. box200: 951 cells of 32 B, bake 77.4 -> 74.9 ms
@@ -1253,9 +1262,9 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
        16-per-record grid in global memory. */
     c->cells_lds = false;
     {
-        const char *cl = getenv("FMGI_CELLS_LDS");
-        if (!grid_cpr_env() && !(cl && atoi(cl) == 0) && gb.J[0] == 1 && gb.J[1] == 1 && gb.J[2] == 1 &&
-            !getenv("FMGI_NO_AXES")) {
+        const char *cl = fmgi_exp_env("FMGI_CELLS_LDS");
+        if (!cpr_forced && !(cl && atoi(cl) == 0) && gb.J[0] == 1 && gb.J[1] == 1 && gb.J[2] == 1 &&
+            !no_axes(c)) {
             for (int cpr : {5, 4}) {
                 GridBuild g = build_grid(fb, cpr);
                 if (g.cells.size() * sizeof(GridCell) <= 32768) {
@@ -1272,9 +1281,9 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     GridBuild gcomp;
     bool try_compact = false;
     {
-        const char *ce = getenv("FMGI_COMPACT");
-        if (c->device != FMGI_HOST_ONLY && !c->cells_lds && !grid_cpr_env() && !(ce && atoi(ce) == 0) &&
-            gb.J[0] == 1 && gb.J[1] == 1 && gb.J[2] == 1 && !getenv("FMGI_NO_AXES") && fb.general.empty() &&
+        const char *ce = fmgi_exp_env("FMGI_COMPACT");
+        if (c->device != FMGI_HOST_ONLY && !c->cells_lds && !cpr_forced && !(ce && atoi(ce) == 0) &&
+            gb.J[0] == 1 && gb.J[1] == 1 && gb.J[2] == 1 && !no_axes(c) && fb.general.empty() &&
             num_walls > 0 && num_walls < 0xFFFF) {
             for (int cpr : {4, 3, 2}) {
                 GridBuild g = build_grid(fb, cpr);
@@ -1306,7 +1315,7 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     const int pairs_bytes = (int)(pairs_img.size() * sizeof(FilterPairHalf));
     c->pair_off_full = (c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size() + 15) & ~15;
     c->himg_full_bytes = c->pair_off_full + pairs_bytes;
-    if (const char *pe = getenv("FMGI_PAIRS")) /* experiments: 0 = no pair image (honoured by FMGI_FILTER_PK=0 builds) */
+    if (const char *pe = fmgi_exp_env("FMGI_PAIRS")) /* experiments: 0 = no pair image (honoured by FMGI_FILTER_PK=0 builds) */
         if (atoi(pe) == 0 && !fmgi_kernels_filter_pk()) c->himg_full_bytes = c->fimg_bytes + c->gimg_bytes + (int)plan_blob.size();
     /* the default instance stages only what it reads: the plane image (a multiple of 64 B) and the pairs */
     c->pair_off = c->gimg_bytes;
@@ -1420,6 +1429,20 @@ FMGI_API int fmgi_set_scene(fmgi_context *c, const fmgi_rect *walls, int num_wal
     c->h_launches.clear();
     c->total_items = 0;
     c->scene_gen++;
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_set_grid_cells_per_record(fmgi_context *c, int cells_per_record) {
+    if (!c || cells_per_record < 0 || cells_per_record > 64) return set_err(FMGI_ERR_ARG, "cells per record 0..64");
+    c->grid_cpr = cells_per_record;
+    return FMGI_OK;
+}
+
+FMGI_API int fmgi_experiments(void) { return FMGI_EXPERIMENTS; }
+
+FMGI_API int fmgi_set_option(fmgi_context *c, int option, int64_t value) {
+    if (!c || option <= 0 || option >= FMGI_OPT_COUNT) return set_err(FMGI_ERR_ARG, "fmgi_set_option: bad option %d", option);
+    c->opt[option] = value;
     return FMGI_OK;
 }
 
@@ -1552,7 +1575,7 @@ static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs,
        (`grecs`): the lane-by-lane stores' instance stages them (then its bake loop reads no global memory at
        all, FMGI_KVAR_STAGED); the rings' instance keeps them in global memory (box200 bake 76.65 -> 77.16 ms
        with them staged at 4 waves/SIMD, profiles/r04/s26). FMGI_GRECS_LDS=0/1 forces (experiments). */
-    const char *ge = getenv("FMGI_GRECS_LDS");
+    const char *ge = fmgi_exp_env("FMGI_GRECS_LDS");
     const bool ov = cells && (ge ? atoi(ge) == 1 : grecs);
     if (groff) *groff = ov ? off : -1;
     if (ov) off += c->grid_entries * 16;
@@ -1567,17 +1590,17 @@ static int stage_bytes(const fmgi_context *c, int kernel, bool rects, bool srcs,
    walks diverge and wait on dependent LDS reads, and example.png baked 2x slower than with the filter
    pass (profiles/r03/s9) */
 static bool grid_axes_scene(const fmgi_context *c) {
-    return c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !getenv("FMGI_NO_AXES");
+    return c->gJ[0] == 1 && c->gJ[1] == 1 && c->gJ[2] == 1 && !no_axes(c);
 }
 static int kernel_instance(const fmgi_context *c, int kernel) {
-    const char *pe = getenv("FMGI_PLAN");
+    const char *pe = fmgi_exp_env("FMGI_PLAN");
     if (kernel == FMGI_KERNEL_HYBRID && c->plan_off >= 0 && pe && atoi(pe) == 1) return kernel | FMGI_KVAR_PLAN;
     return kernel == FMGI_KERNEL_GRID && grid_axes_scene(c) ? (kernel | FMGI_KVAR_AXES) : kernel;
 }
 
 static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool trace) {
     StagePlan p;
-    const char *be = getenv("FMGI_BLOCK");
+    const char *be = fmgi_exp_env("FMGI_BLOCK");
     const int forced_block = (be && atoi(be) >= 64 && atoi(be) <= 1024 && atoi(be) % 64 == 0) ? atoi(be) : 0;
     p.block = forced_block ? forced_block : 256;
     if (kernel == FMGI_KERNEL_EXACT) return p; /* no LDS image: nothing is staged */
@@ -1603,7 +1626,7 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
             return p;
         p = StagePlan{}; /* (does not launch: the general planning below) */
     }
-    const char *se = getenv("FMGI_SRCS_LDS"), *re = getenv("FMGI_RECTS_LDS");
+    const char *se = fmgi_exp_env("FMGI_SRCS_LDS"), *re = fmgi_exp_env("FMGI_RECTS_LDS");
     const bool srcs = c->nsrcs > 0 && !(se && atoi(se) == 0);
     const int rects_mode = re ? atoi(re) : -1; /* -1 auto */
     const int kfn = kernel_instance(c, kernel);
@@ -1626,7 +1649,7 @@ static StagePlan plan_stage(const fmgi_context *c, int kernel, int accum, bool t
     /* the grid cells in LDS: every cell lookup an LDS read instead of an L2 one. The closed boxes' coarse
        grid asks for it (kept only if the wave count holds); FMGI_CELLS_LDS=1 forces it for any grid or
        hybrid scan that fits, 0 turns it off (experiments) */
-    const char *ce = getenv("FMGI_CELLS_LDS");
+    const char *ce = fmgi_exp_env("FMGI_CELLS_LDS");
     /* (only the grid scan reads the staged GridCell copy: ScanHybrid's grid walk reads GridCellF from global
        memory, so staging for it would be dead LDS) */
     const bool cells_forced = ce && atoi(ce) == 1 && kernel == FMGI_KERNEL_GRID;
@@ -1679,7 +1702,7 @@ static int grid_blocks(const fmgi_context *c, int kernel, int accum, bool trace,
        lanes than work items */
     int per_cu = fmgi_bake_resident_blocks(inst >= 0 ? inst : kernel_instance(c, kernel), accum, trace, block, lds);
     if (per_cu <= 0) per_cu = 4;
-    if (const char *pe = getenv("FMGI_BAKE_WG_PER_CU")) /* experiments: leave room for concurrent folds */
+    if (const char *pe = fmgi_exp_env("FMGI_BAKE_WG_PER_CU")) /* experiments: leave room for concurrent folds */
         if (atoi(pe) > 0) per_cu = std::min(per_cu, atoi(pe));
     uint64_t lanes_max = (uint64_t)c->num_cus * per_cu * block;
     uint64_t lanes = std::min<uint64_t>(items, lanes_max);
@@ -1737,12 +1760,13 @@ static uint64_t stream_chunk_items(fmgi_context *c, int sets, int mode) {
    presorted segments / buckets. */
 static int stream_layout(const fmgi_context *c) {
     const int P = (c->num_texels + (1 << FMGI_TILE_BITS) - 1) >> FMGI_TILE_BITS;
-    const char *pre_env = getenv("FMGI_PRESORT");
+    const char *pre_env = fmgi_exp_env("FMGI_PRESORT"); /* experiments: 1 = presorted segments */
     int smode = (P >= 1 && P <= FMGI_PRESORT_MAX_TILES) ? kStreamBuckets : kStreamSliced;
     if (pre_env && P >= 1 && P <= FMGI_PRESORT_MAX_TILES) smode = std::max(0, std::min(2, atoi(pre_env)));
     if (pre_env && atoi(pre_env) == 0) smode = kStreamSliced;
+    if (c->opt[FMGI_OPT_STREAM_LAYOUT] == 0) smode = kStreamSliced; /* tests: the slice-sorted layout */
     if (smode == kStreamBuckets) { /* FMGI_DENSE=1: the dense stream and k_bin instead of the bake's rings */
-        const char *de = getenv("FMGI_DENSE");
+        const char *de = fmgi_exp_env("FMGI_DENSE");
         if (de && atoi(de) == 1) smode = kStreamDense;
     }
     return smode;
@@ -1754,15 +1778,14 @@ static int exec_accum(const fmgi_context *c) {
     if (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamDense) return kAccDense;
     if (c->accum == FMGI_ACCUM_STREAM && stream_layout(c) == kStreamSliced) return kAccSliced;
     if (c->accum != FMGI_ACCUM_STREAM || stream_layout(c) != kStreamBuckets) return c->accum;
-    const char *le = getenv("FMGI_LINES");
+    const char *le = fmgi_exp_env("FMGI_LINES");
     if (le && atoi(le) == 1) return kAccLines;
     /* AUTO: the lane-by-lane stores (AccScatter) when the scene's wall table (and the closed box's grid cells)
        fit in LDS beside the image, so the bake loop reads no global memory and the scattered stores' slow
        completions never hold up a load's s_waitcnt (box200: bake 76.7 -> 69.3 ms at 6 instead of 4 waves per
        SIMD; box2000, whose 2000 walls stay in L2: 132 ms with the rings, 160 with scattered stores; profiles/
        r05/s5). FMGI_SCATTER=0/1 forces either (experiments, tests). */
-    const char *se = getenv("FMGI_SCATTER");
-    if (se) return atoi(se) == 1 ? kAccScatter : kAccBucket;
+    if (c->opt[FMGI_OPT_BUCKET_FILL] >= 0) return c->opt[FMGI_OPT_BUCKET_FILL] ? kAccScatter : kAccBucket; /* tests */
     if (c->compact) return kAccScatter; /* the compact closed box: every table staged (FMGI_KVAR_COMPACT) */
     const size_t tables = (size_t)c->nrects * sizeof(RectLds) + (c->cells_lds ? (size_t)c->grid_cells * sizeof(GridCell) : 0);
     return tables <= 64 * 1024 ? kAccScatter : kAccBucket;
@@ -1799,8 +1822,9 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
        global-memory paths for them are compiled out (FMGI_KVAR_STAGED); FMGI_NO_STAGED=1 (experiments) keeps
        the general one */
     int inst = kernel_instance(c, kernel);
+    /* (the staged and compact instances have no path for rects that are not axis-aligned) */
     if (inst == (FMGI_KERNEL_GRID | FMGI_KVAR_AXES) && sp.rects_off >= 0 && sp.srcs_off >= 0 && sp.cells_off >= 0 &&
-        sp.grecs_off >= 0 && !getenv("FMGI_NO_STAGED"))
+        sp.grecs_off >= 0 && c->ngeneral == 0 && !fmgi_exp_env("FMGI_NO_STAGED"))
         inst |= FMGI_KVAR_STAGED;
     if (inst == (FMGI_KERNEL_GRID | FMGI_KVAR_AXES) && sp.rectc_off >= 0) inst |= FMGI_KVAR_COMPACT;
     /* a closed box built with the coarse LDS grid (5 cells per record) but launched without the cells staged
@@ -1841,7 +1865,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         a.grecs = c->d_grecs;
         a.gridx = c->d_gidx;
         a.grid_axes = grid_axes_scene(c) ? 1 : 0;
-        a.grid_xy_separate = getenv("FMGI_GRID_SEPARATE") ? 1 : 0;
+        a.grid_xy_separate = fmgi_exp_env("FMGI_GRID_SEPARATE") ? 1 : 0;
     } else if (kernel == FMGI_KERNEL_HYBRID) {
         const bool full = hybrid_full(c);
         a.fimg = full ? c->d_himg_full : c->d_himg;
@@ -1973,8 +1997,8 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
        lanes shorten the items' serial photon chains (FMGI_COOP forces a group size: tests) */
     a.coop = 1;
     if (kernel == FMGI_KERNEL_FAST && !trace && c->accum == FMGI_ACCUM_STREAM) {
-        if (const char *ce = getenv("FMGI_COOP")) {
-            const int k = atoi(ce);
+        if (c->opt[FMGI_OPT_COOP] > 0) {
+            const int k = (int)c->opt[FMGI_OPT_COOP];
             a.coop = (k == 2 || k == 4 || k == 8) ? k : 1;
         } else {
             const uint64_t lanes_max =
@@ -1990,7 +2014,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
        sum, so any order gives the same bits. The first bake of a schedule measures (one atomic per item
        into a per-source total); FMGI_FETCH_ORDER=0 turns it off. */
     constexpr int kMaxTabs = 64;
-    const char *fo_env = getenv("FMGI_FETCH_ORDER");
+    const char *fo_env = fmgi_exp_env("FMGI_FETCH_ORDER");
     const bool order_on = !(fo_env && atoi(fo_env) == 0) && c->nsrcs > 0;
     const int ns = c->nsrcs;
     /* only launches of at most 16 items per resident lane reorder (box200's 30 per lane: plain order) */
@@ -2113,11 +2137,11 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     const uint64_t n = e - b;
     const int lanes = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, UINT64_MAX) * block;
     int pipeline = 1;
-    if (const char *pe = getenv("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
+    if (const char *pe = fmgi_exp_env("FMGI_PIPELINE")) pipeline = std::max(1, atoi(pe));
     const int smode = stream_layout(c); /* kStreamBuckets <=> kacc == kAccBucket */
     uint64_t chunk = stream_chunk_items(c, pipeline > 1 ? 2 : 1, smode);
-    if (const char *ce = getenv("FMGI_CHUNK_ITEMS")) /* tests: force several chunks */
-        if (atoll(ce) > 0) chunk = std::min<uint64_t>(chunk, (uint64_t)atoll(ce));
+    if (c->opt[FMGI_OPT_CHUNK_ITEMS] > 0) /* tests: force several chunks */
+        chunk = std::min<uint64_t>(chunk, (uint64_t)c->opt[FMGI_OPT_CHUNK_ITEMS]);
     if (pipeline > 1) chunk = std::min<uint64_t>(chunk, std::max<uint64_t>((n + pipeline - 1) / pipeline, 4 * (uint64_t)lanes));
     chunk = std::max<uint64_t>(chunk, 1);
     const bool overlap = pipeline > 1 && chunk < n;
@@ -2171,7 +2195,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         HIPCHK(hipMemsetAsync(sb.cursor, 0, 16, s)); /* the pool / stream cursor and the dense stream's */
         hipEvent_t t0 = nullptr, t1 = nullptr;
-        if (getenv("FMGI_SHOW_LAUNCH")) /* experiments: the launch shape the planner chose */
+        if (fmgi_exp_env("FMGI_SHOW_LAUNCH")) /* experiments: the launch shape the planner chose */
             fprintf(stderr, "fmgi: bake kernel %d accum %d block %d grid %d lds %zu (staged %d: rects %d srcs %d cells %d)\n",
                     a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, block, grid, fmgi_bake_lds(kernel_instance(c, kernel), kacc, block, a.fimg_bytes, nullptr),
                     a.fimg_bytes, a.rects_off, a.srcs_off, a.cells_off);

@@ -15,6 +15,23 @@
 /* One axis-aligned rectangle as the conservative filter sees it (32 B = one s_load_dwordx8):
    the plane coordinate along its normal's axis a, and centre / half-extent (+ margin) along the two
    other axes u < v. idx = index in the rect list (the exact data is in RectDev[idx]). */
+/* Experiment knobs: FMGI_EXPERIMENTS builds (make experiments -> libflatmatch_gi_exp.so, FMGI_LIB=exp) read the
+   environment variables of the measured-and-rejected paths (dense stream + k_bin, presorted segments, split
+   folds, 8192-texel tiles, per-workgroup tile lines, the floor-plan walk, staging and launch-shape overrides);
+   the product library reads none of them and does not contain those kernel instances. */
+#ifndef FMGI_EXPERIMENTS
+#define FMGI_EXPERIMENTS 0
+#endif
+#include <stdlib.h>
+static inline const char *fmgi_exp_env(const char *name) {
+#if FMGI_EXPERIMENTS
+    return getenv(name);
+#else
+    (void)name;
+    return nullptr;
+#endif
+}
+
 struct FilterRec {
     float plane, cu, hwu, cv, hwv;
     int32_t idx;

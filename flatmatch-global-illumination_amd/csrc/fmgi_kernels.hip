@@ -541,9 +541,10 @@ template <bool Staged = false>
 __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const char *lds, const GridCell &c, float f,
                                                 float uh, float vh, uint32_t qu, uint32_t qv, float &L1, float &L2,
                                                 int &code1, unsigned &ntest) {
+    /* (the closed-box scans' cells: grid_code_or is the hybrid scan's, whose grid walk reads the float cells) */
     ntest += (unsigned)c.count;
-    grid_recq(f, qu, qv, c.qu0, c.qv0, c.idx0 | a.grid_code_or, L1, L2, code1);
-    grid_recq(f, qu, qv, c.qu1, c.qv1, c.idx1 | a.grid_code_or, L1, L2, code1);
+    grid_recq(f, qu, qv, c.qu0, c.qv0, c.idx0, L1, L2, code1);
+    grid_recq(f, qu, qv, c.qu1, c.qv1, c.idx1, L1, L2, code1);
     if (c.count > 2) {
         if (Staged || uni(a.grecs_off) >= 0) { /* the overflow records staged beside the cells */
             typedef float f4v __attribute__((ext_vector_type(4)));
@@ -553,12 +554,12 @@ __device__ __forceinline__ void grid_cell_tests(const BakeArgs &a, const char *l
             const __attribute__((address_space(3))) int *ix = (const __attribute__((address_space(3))) int *)(l + a.gidx_off);
             for (int k = 2; k < c.count; k++) {
                 const f4v r = recs[c.rest + k - 2];
-                grid_rec(f, uh, vh, make_float4(r.x, r.y, r.z, r.w), ix[c.rest + k - 2] | a.grid_code_or, L1, L2, code1);
+                grid_rec(f, uh, vh, make_float4(r.x, r.y, r.z, r.w), ix[c.rest + k - 2], L1, L2, code1);
             }
         } else {
             const float4 *recs = (const float4 *)a.grecs;
             for (int k = 2; k < c.count; k++)
-                grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2] | a.grid_code_or, L1, L2, code1);
+                grid_rec(f, uh, vh, recs[c.rest + k - 2], a.gridx[c.rest + k - 2], L1, L2, code1);
         }
     }
 }
@@ -889,7 +890,7 @@ struct ScanGridT {
             grid_visit<0, true>(a, lds, 0, J0, src, dir, take);
             grid_visit<1, true>(a, lds, 128 * J0, J1, src, dir, take);
             grid_visit<2, true>(a, lds, 128 * (J0 + J1), J2, src, dir, take);
-            for (int g = 0; g < uni(a.ngeneral); g++) {
+            for (int g = 0; g < (Staged ? 0 : uni(a.ngeneral)); g++) { /* (the staged instances: none) */
                 const int idx = a.general[g];
                 if (idx > prev && idx < nxt && exact_on_v(a.rects, idx, src, dir, INFINITY) >= 0) nxt = idx;
             }
@@ -910,6 +911,9 @@ struct ScanGridT {
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
+        /* L2 opaque to the compiler: knowing it infinite, it turns the first record tests' v_med3_f32 into
+           v_max_f32 with canonicalising v_max_f32 x, x, x of both operands (two VALU more per record) */
+        asm volatile("" : "+v"(L2));
         int code1 = -1;
         unsigned ntest = 0;
         if (Axes) {
@@ -928,16 +932,23 @@ struct ScanGridT {
                 grid_xy_merged(a, lds, src, dir, L1, L2, code1, ntest);
             }
         }
-        cptr<int32_t> G = (cptr<int32_t>)a.general;
-        for (int g = 0; g < uni(a.ngeneral); g++) { /* not axis-aligned: exact order-independent tests */
-            const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
-            const float key = (f < 0) ? INFINITY : f;
-            const bool lt = key < L1;
-            L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
-            code1 = lt ? G[g] : code1;
-            L1 = lt ? key : L1;
+        /* rects that are not axis-aligned: exact order-independent tests. The staged and compact instances run
+           only for scenes without them (bake_common): compiled out there, since the loop's global loads made
+           the compiler wait for vmcnt(0) after it, i.e. for the previous iteration's deposit store (gfx9 counts
+           stores in vmcnt), on every scan */
+        if (!Staged) {
+            cptr<int32_t> G = (cptr<int32_t>)a.general;
+            for (int g = 0; g < uni(a.ngeneral); g++) {
+                const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
+                const float key = (f < 0) ? INFINITY : f;
+                const bool lt = key < L1;
+                L2 = __builtin_amdgcn_fmed3f(L1, key, L2);
+                code1 = lt ? G[g] : code1;
+                L1 = lt ? key : L1;
+            }
+            ntest += (unsigned)a.ngeneral;
         }
-        st.tests += ntest + (uint32_t)a.ngeneral;
+        st.tests += ntest;
         st.clk.lap(ST_SCAN1);
         if (L1 == INFINITY) {
             h.best = INFINITY;
@@ -1589,6 +1600,7 @@ using AccSliced = AccStreamT<0>;  /* unsorted codes only (lightmaps of more than
                                      spills made the 30-room layout's bake 16 % slower (profiles/r05/s10) */
 using AccBucket = AccStreamT<2>;  /* per-tile buckets (BakeArgs::presort 2) */
 
+#if FMGI_EXPERIMENTS
 /*
  * The bucket layout written through per-workgroup tile lines (kAccLines). The per-wave rings cost 6 KB of
  * LDS per wave and a register-hungry flush (each lane holds 16 codes while the ring is sorted), which held
@@ -1746,6 +1758,7 @@ struct AccLines {
     }
 };
 
+#endif // FMGI_EXPERIMENTS
 /*
  * The bucket layout written straight from the lanes (kAccScatter). The rings of AccStreamT cost 6 KB of LDS
  * per wave and a flush that holds 16 codes per lane while it sorts them (115 VGPRs): the bake ran at 4 waves
@@ -1883,6 +1896,7 @@ struct AccScatter {
     }
 };
 
+#if FMGI_EXPERIMENTS
 /*
  * The dense stream (kAccDense): the bake only writes, the fold's binning pass (k_bin, fmgi_accum.hip) sorts.
  * At the end of every iteration the depositing lanes of a wave take consecutive slots (ballot + mbcnt) after
@@ -1947,14 +1961,17 @@ struct AccDense {
     }
 };
 
+#endif // FMGI_EXPERIMENTS
 template <class Acc>
 struct HasAppend {
     static constexpr bool value = false;
 };
+#if FMGI_EXPERIMENTS
 template <>
 struct HasAppend<AccDense> {
     static constexpr bool value = true;
 };
+#endif
 
 template <>
 struct HasAppend<AccScatter> {
@@ -1964,10 +1981,12 @@ template <int Mode>
 struct HasAppend<AccStreamT<Mode>> {
     static constexpr bool value = true;
 };
+#if FMGI_EXPERIMENTS
 template <>
 struct HasAppend<AccLines> {
     static constexpr bool value = true;
 };
+#endif
 /* the LDS region of an appending accumulation: the wave's ring (AccStreamT), the workgroup's tile lines
    (AccLines) */
 template <class Acc>
@@ -1978,10 +1997,12 @@ template <>
 __device__ __forceinline__ uint32_t *acc_region<AccBucket>(char *lds, const BakeArgs &a) {
     return (uint32_t *)(lds + a.ring_off) + (threadIdx.x >> 6) * FMGI_RING_STRIDE_BUCKET;
 }
+#if FMGI_EXPERIMENTS
 template <>
 __device__ __forceinline__ uint32_t *acc_region<AccLines>(char *lds, const BakeArgs &a) {
     return (uint32_t *)(lds + a.ring_off);
 }
+#endif
 template <>
 __device__ __forceinline__ uint32_t *acc_region<AccScatter>(char *lds, const BakeArgs &a) {
     return (uint32_t *)(lds + a.ring_off) + (threadIdx.x >> 6) * FMGI_SCATTER_STRIDE;
@@ -2075,15 +2096,19 @@ struct ScanWaves<Scan, decltype((void)Scan::kWaves)> {
 };
 template <class Acc>
 constexpr int acc_min_waves() { return 1; }
+#if FMGI_EXPERIMENTS
 template <>
 constexpr int acc_min_waves<AccLines>() { return 6; }
+#endif
 #ifndef FMGI_SCATTER_WAVES /* AccScatter: the registers of this many waves per SIMD (experiment builds: 4, 5, 6) */
 #define FMGI_SCATTER_WAVES 6
 #endif
 template <>
 constexpr int acc_min_waves<AccScatter>() { return FMGI_SCATTER_WAVES; }
+#if FMGI_EXPERIMENTS
 template <>
 constexpr int acc_min_waves<AccDense>() { return FMGI_SCATTER_WAVES; }
+#endif
 template <class Scan, class Acc, bool TRACE>
 __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     extern __shared__ __attribute__((aligned(16))) char s_img[];
@@ -2455,45 +2480,61 @@ const void *kernel_ptr(bool trace) {
 
 /* accumulation codes: FMGI_ACCUM_FX3 1, STATE 2, NONE 3, STREAM 4 (unsorted / presorted layouts) and the
    internal kAccBucket 5 (STREAM in the per-tile bucket layout) */
+/* (the experiment build's accumulations: the presorted-segment stream, per-workgroup tile lines, the dense
+   stream; the product library has no instance of them and rejects their ids) */
 template <class Scan>
 const void *kernel_acc(int accum, bool trace) {
     if (accum == 2) return kernel_ptr<Scan, AccState>(trace);
     if (accum == 3) return kernel_ptr<Scan, AccNone>(trace);
-    if (accum == 4) return kernel_ptr<Scan, AccStream>(trace);
     if (accum == kAccSliced) return kernel_ptr<Scan, AccSliced>(trace);
     if (accum == kAccBucket) return kernel_ptr<Scan, AccBucket>(trace);
-    if (accum == kAccLines) return kernel_ptr<Scan, AccLines>(trace);
     if (accum == kAccScatter) return kernel_ptr<Scan, AccScatter>(trace);
+#if FMGI_EXPERIMENTS
+    if (accum == 4) return kernel_ptr<Scan, AccStream>(trace);
+    if (accum == kAccLines) return kernel_ptr<Scan, AccLines>(trace);
     if (accum == kAccDense) return kernel_ptr<Scan, AccDense>(trace);
+#else
+    if (accum == 4 || accum == kAccLines || accum == kAccDense) return nullptr;
+#endif
     return kernel_ptr<Scan, AccFx3>(trace);
 }
 
 template <class Scan>
-void launch_acc(const BakeArgs &a, int accum, bool trace, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
+bool launch_acc(const BakeArgs &a, int accum, bool trace, dim3 grid, dim3 block, size_t lds, hipStream_t s) {
     if (accum == 2) launch3<Scan, AccState>(a, trace, grid, block, lds, s);
     else if (accum == 3) launch3<Scan, AccNone>(a, trace, grid, block, lds, s);
-    else if (accum == 4) launch3<Scan, AccStream>(a, trace, grid, block, lds, s);
     else if (accum == kAccSliced) launch3<Scan, AccSliced>(a, trace, grid, block, lds, s);
     else if (accum == kAccBucket) launch3<Scan, AccBucket>(a, trace, grid, block, lds, s);
-    else if (accum == kAccLines) launch3<Scan, AccLines>(a, trace, grid, block, lds, s);
     else if (accum == kAccScatter) launch3<Scan, AccScatter>(a, trace, grid, block, lds, s);
+#if FMGI_EXPERIMENTS
+    else if (accum == 4) launch3<Scan, AccStream>(a, trace, grid, block, lds, s);
+    else if (accum == kAccLines) launch3<Scan, AccLines>(a, trace, grid, block, lds, s);
     else if (accum == kAccDense) launch3<Scan, AccDense>(a, trace, grid, block, lds, s);
+#else
+    else if (accum == 4 || accum == kAccLines || accum == kAccDense) return false;
+#endif
     else launch3<Scan, AccFx3>(a, trace, grid, block, lds, s);
+    return true;
 }
 
 const void *bake_kernel(int kernel, int accum, bool trace) {
     if (kernel == FMGI_KERNEL_FAST_COOP)
         return accum == kAccBucket ? kernel_ptr<ScanFastCoop, AccBucket>(false)
-               : accum == kAccLines ? kernel_ptr<ScanFastCoop, AccLines>(false)
                : accum == kAccScatter ? kernel_ptr<ScanFastCoop, AccScatter>(false)
-               : accum == kAccDense ? kernel_ptr<ScanFastCoop, AccDense>(false)
                : accum == kAccSliced ? kernel_ptr<ScanFastCoop, AccSliced>(false)
-                                    : kernel_ptr<ScanFastCoop, AccStream>(false);
+#if FMGI_EXPERIMENTS
+               : accum == kAccLines ? kernel_ptr<ScanFastCoop, AccLines>(false)
+               : accum == kAccDense ? kernel_ptr<ScanFastCoop, AccDense>(false)
+               : accum == 4 ? kernel_ptr<ScanFastCoop, AccStream>(false)
+#endif
+                                    : nullptr;
     if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_COMPACT)) /* the lane-by-lane stores only (bake_common) */
         return accum == kAccScatter ? kernel_ptr<ScanGridAxesCompact, AccScatter>(trace) : nullptr;
     if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) return kernel_acc<ScanGridAxesStaged>(accum, trace);
     if (kernel == (2 | FMGI_KVAR_AXES)) return kernel_acc<ScanGridAxes>(accum, trace);
+#if FMGI_EXPERIMENTS
     if (kernel == (4 | FMGI_KVAR_PLAN)) return kernel_acc<ScanHybridPlan>(accum, trace);
+#endif
     kernel &= ~(FMGI_KVAR_AXES | FMGI_KVAR_PLAN | FMGI_KVAR_STAGED);
     if (kernel == 2) return kernel_acc<ScanGrid>(accum, trace);
     if (kernel == 4) return kernel_acc<ScanHybrid>(accum, trace);
@@ -2510,7 +2551,9 @@ int fmgi_kernels_filter_pk() { return FMGI_FILTER_PK; }
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
     const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
     if (ring_off) *ring_off = (int)img;
+#if FMGI_EXPERIMENTS
     if (accum == kAccLines) return img + (size_t)FMGI_LINES_DWORDS * 4;
+#endif
     if (accum == kAccScatter) return img + (size_t)(block / 64) * FMGI_SCATTER_STRIDE * 4;
     if (accum == kAccBucket) return img + (size_t)(block / 64) * FMGI_RING_STRIDE_BUCKET * 4;
     return img + ((accum == 4 || accum == kAccSliced) ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
@@ -2552,35 +2595,38 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         const hipError_t e = bake_lds_attr(bake_kernel(kernel, accum, trace), lds);
         if (e != hipSuccess) return e;
     }
+    bool ok = true;
     if (kernel == FMGI_KERNEL_FAST_COOP) {
-        if ((accum != 4 && accum != kAccBucket && accum != kAccLines && accum != kAccScatter && accum != kAccDense &&
-             accum != kAccSliced) ||
-            trace)
-            return hipErrorInvalidValue;
+        if (trace || !bake_kernel(kernel, accum, false)) return hipErrorInvalidValue;
         if (accum == kAccBucket) launch3<ScanFastCoop, AccBucket>(a, false, grid, blk, lds, s);
         else if (accum == kAccScatter) launch3<ScanFastCoop, AccScatter>(a, false, grid, blk, lds, s);
-        else if (accum == kAccDense) launch3<ScanFastCoop, AccDense>(a, false, grid, blk, lds, s);
         else if (accum == kAccSliced) launch3<ScanFastCoop, AccSliced>(a, false, grid, blk, lds, s);
+#if FMGI_EXPERIMENTS
+        else if (accum == kAccDense) launch3<ScanFastCoop, AccDense>(a, false, grid, blk, lds, s);
         else if (accum == kAccLines) launch3<ScanFastCoop, AccLines>(a, false, grid, blk, lds, s);
         else launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
     } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */
-        launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);
+        ok = launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);
+#endif
     } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
-        launch_acc<ScanHybrid>(a, accum, trace, grid, blk, lds, s);
+        ok = launch_acc<ScanHybrid>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_COMPACT)) { /* closed box, the compact tables in LDS */
         if (accum != kAccScatter) return hipErrorInvalidValue;
         launch3<ScanGridAxesCompact, AccScatter>(a, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) { /* closed box, every table in LDS */
-        launch_acc<ScanGridAxesStaged>(a, accum, trace, grid, blk, lds, s);
+        ok = launch_acc<ScanGridAxesStaged>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == (2 | FMGI_KVAR_AXES)) { /* FMGI_KERNEL_GRID, closed box */
-        launch_acc<ScanGridAxes>(a, accum, trace, grid, blk, lds, s);
+        ok = launch_acc<ScanGridAxes>(a, accum, trace, grid, blk, lds, s);
     } else if ((kernel & ~FMGI_KVAR_AXES) == 2) { /* FMGI_KERNEL_GRID */
-        launch_acc<ScanGrid>(a, accum, trace, grid, blk, lds, s);
+        ok = launch_acc<ScanGrid>(a, accum, trace, grid, blk, lds, s);
     } else if (kernel == 1) { /* FMGI_KERNEL_FAST */
-        launch_acc<ScanFast>(a, accum, trace, grid, blk, lds, s);
+        ok = launch_acc<ScanFast>(a, accum, trace, grid, blk, lds, s);
+    } else if ((kernel & 0xF) == 0) {
+        ok = launch_acc<ScanExact>(a, accum, trace, grid, blk, lds, s);
     } else {
-        launch_acc<ScanExact>(a, accum, trace, grid, blk, lds, s);
+        ok = false;
     }
+    if (!ok) return hipErrorInvalidValue; /* no instance (an experiment build's kernel or accumulation) */
     return hipGetLastError();
 }
 

@@ -193,6 +193,17 @@ class Context:
         check(self.lib.fmgi_get_timing(self.h, C.byref(t)), "fmgi_get_timing")
         return t.as_dict()
 
+    def set_option(self, name: str, value: int):
+        """fmgi_set_option: one of _lib.OPTIONS (chunk_items, pool_limit, stream_layout, bucket_fill, wide_tiles,
+        coop, no_axes); takes effect at the next bake (no_axes: the next set_scene)."""
+        from ._lib import OPTIONS
+
+        check(self.lib.fmgi_set_option(self.h, OPTIONS[name], int(value)), "fmgi_set_option")
+
+    def set_grid_cells_per_record(self, n: int):
+        """The grid's cells per record for the next set_scene (0: the product's choice)."""
+        check(self.lib.fmgi_set_grid_cells_per_record(self.h, int(n)), "fmgi_set_grid_cells_per_record")
+
     def grid_tables(self) -> dict:
         """FMGI_KERNEL_GRID's plane/cell/record tables (include/flatmatch_gi.h fmgi_grid_copy)."""
         sz = np.zeros(5, np.int32)
@@ -287,6 +298,11 @@ def make_geometry(sc: Scene, texels: np.ndarray):
     g.numTexels = sc.num_texels
     g.texels = texels.ctypes.data
     return g, keep
+
+
+def experiments() -> bool:
+    """Whether the loaded library is the experiment build (reads the experiment knobs)."""
+    return bool(load().fmgi_experiments())
 
 
 def dropin_release():

@@ -7,7 +7,8 @@ import os
 
 PKG_DIR = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 # FMGI_LIB=<name> selects a profiling/experiment build libflatmatch_gi_<name>.so (make -C <pkg> timing,
-# make -C <pkg> variant VNAME=<name> VFLAGS=...); the product and every test use libflatmatch_gi.so
+# make -C <pkg> experiments (FMGI_LIB=exp: the experiment knobs), make -C <pkg> variant VNAME=<name> VFLAGS=...);
+# the product and every test use libflatmatch_gi.so
 LIB_PATH = os.path.join(PKG_DIR, f"libflatmatch_gi_{os.environ['FMGI_LIB']}.so" if os.environ.get("FMGI_LIB")
                         else "libflatmatch_gi.so")
 
@@ -41,6 +42,9 @@ EXPORTS = (
     "fmgi_device_sincosf_library",
     "fmgi_device_unit",
     "fmgi_grid_sizes",
+    "fmgi_set_grid_cells_per_record",
+    "fmgi_experiments",
+    "fmgi_set_option",
     "fmgi_grid_copy",
     "fmgi_plan_copy",
     "fmgi_filter_copy",
@@ -72,6 +76,9 @@ ACCUM_FX3 = 1
 ACCUM_STATE = 2
 ACCUM_NONE = 3  # profiling only: deposits discarded
 ACCUM_STREAM = 4
+# fmgi_set_option (include/flatmatch_gi.h): tests' handles on product paths a scene would not take
+OPTIONS = {"chunk_items": 1, "pool_limit": 2, "stream_layout": 3, "bucket_fill": 4, "wide_tiles": 5, "coop": 6,
+           "no_axes": 7}
 
 
 class FmgiError(RuntimeError):
@@ -193,6 +200,9 @@ def load() -> C.CDLL:
         "fmgi_device_sincosf_library": (C.c_int, [vp, vp, vp, vp, i64]),
         "fmgi_device_unit": (C.c_int, [vp, C.c_int, vp, vp, vp, i64]),
         "fmgi_grid_sizes": (C.c_int, [vp, vp]),
+        "fmgi_set_grid_cells_per_record": (C.c_int, [vp, C.c_int]),
+        "fmgi_experiments": (C.c_int, []),
+        "fmgi_set_option": (C.c_int, [vp, C.c_int, C.c_int64]),
         "fmgi_get_stage_cycles": (C.c_int, [vp, vp]),
         "fmgi_auto_kernel": (C.c_int, [vp]),
         "fmgi_set_timing": (C.c_int, [vp, C.c_int]),

@@ -278,6 +278,30 @@ int fmgi_trace_items(fmgi_context *ctx, uint64_t item_begin, uint64_t item_end, 
      recs[4 * sizes[4]], idx[sizes[4]]: the overflow records (entries 3..count of every cell) and their
        rect indices. */
 int fmgi_grid_sizes(const fmgi_context *ctx, int32_t sizes[5]);
+/* The grid's cells per record for the next fmgi_set_scene of ctx (0, the default: the product's choice, 16,
+   or the coarse LDS grids of the closed boxes); tests use it to check the grids those choices build. */
+int fmgi_set_grid_cells_per_record(fmgi_context *ctx, int cells_per_record);
+/* 1 in the experiment build (make experiments -> libflatmatch_gi_exp.so), whose experiment knobs
+   (environment variables of measured-and-rejected paths) it reads; 0 in the product library. */
+int fmgi_experiments(void);
+/* Per-context handles on product paths that a given scene or launch size would not take, for tests (each
+   takes effect at the next bake; FMGI_OPT_NO_AXES at the next fmgi_set_scene):
+     FMGI_OPT_CHUNK_ITEMS   > 0: at most this many work items per STREAM chunk (several chunks per call)
+     FMGI_OPT_POOL_LIMIT    > 0: at most this many bucket-pool blocks (the exact atomic fallback takes the rest)
+     FMGI_OPT_STREAM_LAYOUT 0: the slice-sorted stream (lightmaps of more than 63 tiles); -1: by the scene
+     FMGI_OPT_BUCKET_FILL   0: per-wave LDS rings, 1: lane-by-lane stores; -1: by the tables' LDS fit
+     FMGI_OPT_WIDE_TILES    0 / 1: 2048- / 4096-texel bucket tiles; -1: by the launch size
+     FMGI_OPT_COOP          2, 4, 8: lanes per work item of ScanFast's small launches; 0: by the launch size
+     FMGI_OPT_NO_AXES       1: closed boxes through the general grid instance (its sorted <= 4-slot phase 1) */
+#define FMGI_OPT_CHUNK_ITEMS 1
+#define FMGI_OPT_POOL_LIMIT 2
+#define FMGI_OPT_STREAM_LAYOUT 3
+#define FMGI_OPT_BUCKET_FILL 4
+#define FMGI_OPT_WIDE_TILES 5
+#define FMGI_OPT_COOP 6
+#define FMGI_OPT_NO_AXES 7
+#define FMGI_OPT_COUNT 8
+int fmgi_set_option(fmgi_context *ctx, int option, int64_t value);
 /* Profiling builds only (make timing -> libflatmatch_gi_timing.so, -DFMGI_STAGE_TIMING): shader-clock
    cycles summed over waves per bake-loop stage {start, sample, scan phase 1, phase 2, fallback, hit,
    append}, since the last fmgi_reset_stats; all zero in the normal library. */

@@ -163,12 +163,10 @@ def test_config5_full_size_properties_and_late_window(torch_cuda, box2000, offse
     assert st["deposits"] + st["escapes"] == st["scans"]
     assert st["stream_overflow"] == 0
     assert st["exact_rescans"] > 0
-    os.environ["FMGI_CHUNK_ITEMS"] = "1700000"  # ~3 chunks per half
-    try:
-        h1 = _bake_gpu(torch_cuda, ctx, 0, n // 2)
-        h2 = _bake_gpu(torch_cuda, ctx, n // 2, n)
-    finally:
-        os.environ.pop("FMGI_CHUNK_ITEMS", None)
+    ctx.set_option("chunk_items", 1_700_000)  # ~3 chunks per half
+    h1 = _bake_gpu(torch_cuda, ctx, 0, n // 2)
+    h2 = _bake_gpu(torch_cuda, ctx, n // 2, n)
+    ctx.set_option("chunk_items", 0)
     assert np.array_equal(full, h1 + h2)
     ctx.close()
     fx = _ctx(box2000, spa, offsets, fmgi.ACCUM_FX3)
@@ -200,12 +198,10 @@ def test_config4_full_size_properties_and_late_window(torch_cuda, box200, offset
     assert st["deposits"] + st["escapes"] == st["scans"]
     assert st["stream_overflow"] == 0
     assert int(full[:, :3].astype(np.float64).sum()) >= st["deposits"] * 3 * (2**25 // 4)
-    os.environ["FMGI_CHUNK_ITEMS"] = "17000000"  # ~3 chunks per half through one buffer set
-    try:
-        h1 = _bake_gpu(torch_cuda, ctx, 0, n // 2)
-        h2 = _bake_gpu(torch_cuda, ctx, n // 2, n)
-    finally:
-        os.environ.pop("FMGI_CHUNK_ITEMS", None)
+    ctx.set_option("chunk_items", 17_000_000)  # ~3 chunks per half through one buffer set
+    h1 = _bake_gpu(torch_cuda, ctx, 0, n // 2)
+    h2 = _bake_gpu(torch_cuda, ctx, n // 2, n)
+    ctx.set_option("chunk_items", 0)
     assert np.array_equal(full, h1 + h2)
     assert ctx.stats()["stream_overflow"] == 0
     # exact window: the last 4,096 items (launches 3905-3906), lightmap and per-photon traces
@@ -279,16 +275,13 @@ def test_cooperative_lanes_config1_exact(torch_cuda, example_scene, offsets, coo
     L = O.schedule_with_offsets(example_scene, spa, offsets)
     olm, ost = O.bake(example_scene, L)
     olm2, _ = O.bake(example_scene, L, 3, 1004)
-    os.environ["FMGI_COOP"] = coop
-    try:
-        ctx = _ctx(example_scene, spa, offsets)
-        ctx.reset_stats()
-        lm = _bake_gpu(torch_cuda, ctx, 0, ctx.total_items, fmgi.KERNEL_FAST)
-        st = ctx.stats()
-        lm2 = _bake_gpu(torch_cuda, ctx, 3, 1004, fmgi.KERNEL_FAST)
-        ctx.close()
-    finally:
-        os.environ.pop("FMGI_COOP", None)
+    ctx = _ctx(example_scene, spa, offsets)
+    ctx.set_option("coop", int(coop))
+    ctx.reset_stats()
+    lm = _bake_gpu(torch_cuda, ctx, 0, ctx.total_items, fmgi.KERNEL_FAST)
+    st = ctx.stats()
+    lm2 = _bake_gpu(torch_cuda, ctx, 3, 1004, fmgi.KERNEL_FAST)
+    ctx.close()
     assert np.array_equal(lm[:, :3], olm)
     assert np.array_equal(lm2[:, :3], olm2)
     for k in ("photons", "scans", "deposits", "escapes"):
@@ -307,17 +300,14 @@ def test_cooperative_lanes_with_general_rects_exact(torch_cuda, offsets, coop):
     L = O.schedule_with_offsets(sc, spa, offsets)
     b, e = 0, 3000
     olm, ost = O.bake(sc, L, b, e)
+    ctx = _ctx(sc, spa, offsets)
     if coop != "1":
-        os.environ["FMGI_COOP"] = coop
-    try:
-        ctx = _ctx(sc, spa, offsets)
-        assert ctx.auto_kernel in (fmgi.KERNEL_FAST, fmgi.KERNEL_GRID, fmgi.KERNEL_HYBRID)
-        ctx.reset_stats()
-        lm = _bake_gpu(torch_cuda, ctx, b, e, fmgi.KERNEL_FAST)
-        st = ctx.stats()
-        ctx.close()
-    finally:
-        os.environ.pop("FMGI_COOP", None)
+        ctx.set_option("coop", int(coop))
+    assert ctx.auto_kernel in (fmgi.KERNEL_FAST, fmgi.KERNEL_GRID, fmgi.KERNEL_HYBRID)
+    ctx.reset_stats()
+    lm = _bake_gpu(torch_cuda, ctx, b, e, fmgi.KERNEL_FAST)
+    st = ctx.stats()
+    ctx.close()
     assert np.array_equal(lm[:, :3], olm)
     for k in ("photons", "scans", "deposits", "escapes"):
         assert st[k] == ost[k], k

@@ -101,31 +101,30 @@ def test_per_photon_traces_boxes(torch_cuda, box200, box2000, offsets, kernel):
 
 
 def test_box_traces_without_axes_mode(torch_cuda, box200, offsets):
-    """The closed boxes use ScanGrid's one-plane-per-class phase 1; FMGI_NO_AXES=1 routes them through
+    """The closed boxes use ScanGrid's one-plane-per-class phase 1; FMGI_OPT_NO_AXES routes them through
     the sorted <= 4-slot phase 1 instead, which no other scene here reaches: same traces."""
-    os.environ["FMGI_NO_AXES"] = "1"
-    try:
-        spa = 172_413_793
-        L = _oracle_plan(box200, spa, offsets)
-        ctx = _ctx(box200, spa, offsets)
-        _compare_traces(box200, ctx, L, 3000, 3128, fmgi.KERNEL_GRID)
-        lm = _bake_gpu(torch_cuda, ctx, 5_000, 25_000, fmgi.KERNEL_GRID)
-        olm, _ = O.bake(box200, L, 5_000, 25_000)
-        assert np.array_equal(lm[:, :3], olm)
-        ctx.close()
-    finally:
-        os.environ.pop("FMGI_NO_AXES", None)
+    spa = 172_413_793
+    L = _oracle_plan(box200, spa, offsets)
+    ctx = fmgi.Context(0)
+    ctx.set_option("no_axes", 1)
+    ctx.set_scene(box200)
+    ctx.plan(spa, rng_offsets=offsets)
+    _compare_traces(box200, ctx, L, 3000, 3128, fmgi.KERNEL_GRID)
+    lm = _bake_gpu(torch_cuda, ctx, 5_000, 25_000, fmgi.KERNEL_GRID)
+    olm, _ = O.bake(box200, L, 5_000, 25_000)
+    assert np.array_equal(lm[:, :3], olm)
+    ctx.close()
 
 
 def test_layout_traces_with_floor_plan(torch_cuda, example_scene, offsets):
     """The hybrid scan's walls through the packed wall-pair filter (default, FMGI_FILTER_PK=1:
-    filter_pairs over the pair image) and through the floor-plan walk (FMGI_PLAN=1, plan_walls): both
-    give the oracle's traces and lightmap."""
+    filter_pairs over the pair image) and, in the experiment build, through the floor-plan walk (FMGI_PLAN=1,
+    plan_walls): both give the oracle's traces and lightmap."""
     spa = 6_500_000
     L = _oracle_plan(example_scene, spa, offsets)
     ctx = _ctx(example_scene, spa, offsets)
     olm, _ = O.bake(example_scene, L, 40_000, 52_000)
-    for env in ("0", "1"):
+    for env in ("0", "1") if fmgi.experiments() else ("0",):
         os.environ["FMGI_PLAN"] = env
         try:
             _compare_traces(example_scene, ctx, L, 41_000, 41_128, fmgi.KERNEL_HYBRID)
@@ -171,74 +170,81 @@ def test_lightmap_box_prefix_exact(torch_cuda, box200, box2000, offsets, kernel,
         ctx.close()
 
 
-FOLD_LAYOUTS = {  # stream layout -> the environment that selects it
-    "buckets_ring": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "0", "FMGI_DENSE": "0"},
-    "buckets_scatter": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_DENSE": "0"},
+# stream layout -> the context options that select it (fmgi_set_option; the product library's layouts)
+FOLD_LAYOUTS = {
+    "buckets_ring": {"bucket_fill": 0, "wide_tiles": 0},
+    "buckets_scatter": {"bucket_fill": 1, "wide_tiles": 0},
+    "buckets_scatter_wide": {"bucket_fill": 1, "wide_tiles": 1},
+    "buckets_ring_wide": {"bucket_fill": 0, "wide_tiles": 1},
+    "sliced": {"stream_layout": 0},
+}
+# ... and the experiment build's (make experiments, FMGI_LIB=exp: its environment knobs), skipped otherwise
+EXP_LAYOUTS = {
     "dense_bin": {"FMGI_PRESORT": "2", "FMGI_DENSE": "1"},
-    "buckets_scatter_wide": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_WIDE_TILES": "1"},
-    "buckets_ring_wide": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "0", "FMGI_WIDE_TILES": "1"},
     "dense_bin_wide": {"FMGI_PRESORT": "2", "FMGI_DENSE": "1", "FMGI_WIDE_TILES": "1"},
     # wide bucket tiles folded as 2 or 4 narrower fold tiles that read the same blocks
-    "buckets_scatter_wide_split2": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_WIDE_TILES": "1",
-                                    "FMGI_FOLD_SPLIT": "2"},
-    "buckets_scatter_w13_split2": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "1", "FMGI_WIDE_TILES": "13",
-                                   "FMGI_FOLD_SPLIT": "2"},
-    "buckets_ring_w13_split4": {"FMGI_PRESORT": "2", "FMGI_SCATTER": "0", "FMGI_WIDE_TILES": "13",
-                                "FMGI_FOLD_SPLIT": "4"},
+    "buckets_scatter_wide_split2": {"FMGI_WIDE_TILES": "1", "FMGI_FOLD_SPLIT": "2"},
+    "buckets_scatter_w13_split2": {"FMGI_WIDE_TILES": "13", "FMGI_FOLD_SPLIT": "2"},
     "presorted": {"FMGI_PRESORT": "1"},
-    "sliced": {"FMGI_PRESORT": "0", "FMGI_PACKED_RUNS": "0"},
     "sliced_packed": {"FMGI_PRESORT": "0", "FMGI_PACKED_RUNS": "1"},
+    "fold_carry": {"FMGI_FOLD_CARRY": "2", "FMGI_WIDE_TILES": "1"},
 }
-FOLD_ENV = sorted({k for v in FOLD_LAYOUTS.values() for k in v} | {"FMGI_POOL_LIMIT", "FMGI_CHUNK_ITEMS"})
+EXP_ENV = sorted({k for v in EXP_LAYOUTS.values() for k in v})
 
 
-def _set_layout(name):
-    for k in FOLD_ENV:
+def _layout_ctx(name, sc, spa, offsets):
+    """a STREAM context on layout `name` (FOLD_LAYOUTS options, or EXP_LAYOUTS environment)"""
+    for k in EXP_ENV:
         os.environ.pop(k, None)
-    os.environ.update(FOLD_LAYOUTS[name])
+    if name in EXP_LAYOUTS:
+        if not fmgi.experiments():
+            pytest.skip("an experiment build's layout (make experiments; FMGI_LIB=exp)")
+        os.environ.update(EXP_LAYOUTS[name])
+    ctx = _ctx(sc, spa, offsets, fmgi.ACCUM_STREAM)
+    for k, v in FOLD_LAYOUTS.get(name, {}).items():
+        ctx.set_option(k, v)
+    return ctx
 
 
-@pytest.mark.parametrize("layout", sorted(FOLD_LAYOUTS))
+@pytest.mark.parametrize("layout", sorted(FOLD_LAYOUTS) + sorted(EXP_LAYOUTS))
 def test_stream_fold_orders_exact(torch_cuda, box200, example_scene, offsets, layout):
     """Every STREAM layout gives the oracle's lightmap: per-tile buckets (the default for lightmaps of at most
     63 fold tiles) filled through the bake's per-wave LDS rings (buckets_ring) or lane by lane (buckets_scatter),
-    the bake's dense code stream binned into buckets by k_bin (dense_bin), the bake-side presorted segments, and
-    the slice-sorted stream (its runs summed one at a time, or packed 16 slices to a wave as for lightmaps of more
-    than 128 tiles); the bucket layouts also with wide (4096- or 8192-texel) tiles, folded whole or as 2 or 4
-    narrower fold tiles that each read every block of the bucket; for full-ring flushes and the partial rings /
-    blocks at the end of a launch."""
-    _set_layout(layout)
+    with 2048- or 4096-texel tiles, and the slice-sorted stream (lightmaps of more than 63 tiles); for full-ring
+    flushes and the partial rings / blocks at the end of a launch. The experiment build's layouts (the dense
+    stream binned by k_bin, split folds, 8192-texel tiles, presorted segments, packed slice runs, the fold's
+    carry words) when that build is loaded."""
     try:
         for sc, spa, lo, hi in ((box200, 172_413_793, 7_000, 27_000), (example_scene, 65_000, 0, 300)):
             L = _oracle_plan(sc, spa, offsets)
-            ctx = _ctx(sc, spa, offsets, fmgi.ACCUM_STREAM)
+            ctx = _layout_ctx(layout, sc, spa, offsets)
             lm = _bake_gpu(torch_cuda, ctx, lo, hi, fmgi.KERNEL_AUTO)
             olm, _ = O.bake(sc, L, lo, hi)
             assert np.array_equal(lm[:, :3], olm), sc.name
             assert ctx.stats()["stream_overflow"] == 0
             ctx.close()
     finally:
-        for k in FOLD_ENV:
+        for k in EXP_ENV:
             os.environ.pop(k, None)
 
 
 @pytest.mark.parametrize("layout", ["buckets_ring", "buckets_scatter", "dense_bin"])
 def test_bucket_pool_exhaustion_falls_back_exactly(torch_cuda, box200, offsets, layout):
-    """A bucket pool that runs out (FMGI_POOL_LIMIT caps it at 64 blocks, far fewer than the bake needs) sends
-    the rest of the codes through device atomics into the int64 lightmap (the bake's bucket_atomic, k_bin's
-    bin_atomic), whichever way the buckets are filled: the lightmap still equals the oracle's."""
-    _set_layout(layout)
-    os.environ["FMGI_POOL_LIMIT"] = "64"
+    """A bucket pool that runs out (FMGI_OPT_POOL_LIMIT caps it at 64 blocks, far fewer than the bake needs)
+    sends the rest of the codes through device atomics into the int64 lightmap (the bake's bucket_atomic; the
+    experiment build's k_bin: bin_atomic), whichever way the buckets are filled: the lightmap still equals the
+    oracle's."""
     try:
         spa = 172_413_793
         L = _oracle_plan(box200, spa, offsets)
-        ctx = _ctx(box200, spa, offsets, fmgi.ACCUM_STREAM)
+        ctx = _layout_ctx(layout, box200, spa, offsets)
+        ctx.set_option("pool_limit", 64)
         lm = _bake_gpu(torch_cuda, ctx, 2_000, 6_000, fmgi.KERNEL_AUTO)
         olm, _ = O.bake(box200, L, 2_000, 6_000)
         assert np.array_equal(lm[:, :3], olm)
         ctx.close()
     finally:
-        for k in FOLD_ENV:
+        for k in EXP_ENV:
             os.environ.pop(k, None)
 
 
@@ -255,19 +261,19 @@ def test_split_invariance_and_determinism_full_size(torch_cuda, box200, offsets)
     c = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
     ctx.set_accumulation(fmgi.ACCUM_STREAM)
     d = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)  # one memory-sized chunk
-    os.environ["FMGI_CHUNK_ITEMS"] = "3000000"  # four chunks through one buffer set ...
-    try:
-        e = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
-        os.environ["FMGI_PIPELINE"] = "3"  # ... and with each fold beside the next chunk's bake
-        f = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
-    finally:
-        os.environ.pop("FMGI_CHUNK_ITEMS", None)
-        os.environ.pop("FMGI_PIPELINE", None)
-    os.environ["FMGI_PRESORT"] = "0"  # the slice-sorted fold (lightmaps of more than 63 fold tiles)
-    try:
-        g = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
-    finally:
-        os.environ.pop("FMGI_PRESORT", None)
+    ctx.set_option("chunk_items", 3_000_000)  # four chunks through one buffer set ...
+    e = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+    f = e
+    if fmgi.experiments():  # ... and (experiment build) with each fold beside the next chunk's bake
+        os.environ["FMGI_PIPELINE"] = "3"
+        try:
+            f = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+        finally:
+            os.environ.pop("FMGI_PIPELINE", None)
+    ctx.set_option("chunk_items", 0)
+    ctx.set_option("stream_layout", 0)  # the slice-sorted fold (lightmaps of more than 63 fold tiles)
+    g = _bake_gpu(torch_cuda, ctx, 0, n, fmgi.KERNEL_GRID)
+    ctx.set_option("stream_layout", -1)
     d1 = _bake_gpu(torch_cuda, ctx, 0, 12_345, fmgi.KERNEL_GRID)
     d2 = _bake_gpu(torch_cuda, ctx, 12_345, n, fmgi.KERNEL_GRID)
     assert np.array_equal(a, b1 + b2)

@@ -13,8 +13,9 @@ import pytest
 import fmgi
 
 
-def _tables(sc):
+def _tables(sc, cells_per_record=0):
     ctx = fmgi.Context(-1)
+    ctx.set_grid_cells_per_record(cells_per_record)
     ctx.set_scene(sc)
     t = ctx.grid_tables()
     f = ctx.filter_image()["recs"]
@@ -211,12 +212,11 @@ def test_grid_is_small_and_selective(box200, box2000):
 
 
 @pytest.mark.parametrize("cpr", [4, 3, 2])
-def test_compact_grids_cover_and_hold_four_records(cpr, box2000, monkeypatch):
+def test_compact_grids_cover_and_hold_four_records(cpr, box2000):
     """The grids the compact closed-box tables index (fmgi_api.cpp build_compact, BASELINE config 5: 4, 3 or 2
     cells per record, each cell's records as up to four u16 indices): the coverage property of every grid, and
     no box2000 cell of more than four records, so every cell fits its CellC."""
-    monkeypatch.setenv("FMGI_GRID_CPR", str(cpr))
-    t = _tables(box2000)
+    t = _tables(box2000, cpr)
     rng = np.random.default_rng(11 + cpr)
     n = 0
     planes = _planes(t)

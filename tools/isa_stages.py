@@ -39,6 +39,8 @@ STAGE_OF_FUNC = [
     ("coop_merge", "fallback (rare)"),
     ("alloc", "pool block allocation (rare)"),
     ("locate_item", "work-item fetch (rare)"),
+    ("exact_on_v", "fallback (rare)"),
+    ("intersect_exact", "fallback (rare)"),
     ("intersect_exact_uv", "phase 2: exact intersects()"),
     ("exact_hit_rec", "phase 2: record fields"),
     ("exact_hit_compact", "phase 2: record fields"),
@@ -56,6 +58,7 @@ STAGE_OF_FUNC = [
     ("trunc_div_inv", "tile index"),
     ("tile_uv", "tile index"),
     ("append", "deposit code: tile word + store"),
+    ("scan", "phase 1/2 glue (winner, separation test)"),
     ("load_src", "emission: emitter fields"),
     ("src_fields", "emission: emitter fields"),
 ]
@@ -128,11 +131,12 @@ def main():
     vgpr = [l for l in syms.splitlines() if name + ".num_vgpr" in l]
     dis = subprocess.run([f"{LLVM}/llvm-objdump", "-d", "--no-show-raw-insn", f"--start-address={start}",
                           f"--stop-address={start + size}", a.obj], capture_output=True, text=True, check=True).stdout
-    insts = []  # (addr, mnemonic, operands)
+    insts = []  # (addr, mnemonic, operands, branch target address or None)
     for l in dis.splitlines():
         m = re.match(r"\s+(\S+)\s*(.*?)\s*//\s*([0-9A-F]+):", l)
         if m:
-            insts.append((int(m.group(3), 16), m.group(1), m.group(2)))
+            t = re.search(r"<[^>]*\+0x([0-9a-f]+)>", l) if m.group(1).startswith(("s_cbranch", "s_branch")) else None
+            insts.append((int(m.group(3), 16), m.group(1), m.group(2), start + int(t.group(1), 16) if t else None))
     addrs = "\n".join(hex(x[0]) for x in insts) + "\n"
     out = subprocess.run([f"{LLVM}/llvm-symbolizer", f"--obj={a.obj}", "--inlining", "--functions=short"],
                          input=addrs, capture_output=True, text=True, check=True).stdout
@@ -152,29 +156,17 @@ def main():
     chains = [c for c in chains if c][: len(insts)]
     src = open(os.path.join(PKG, "csrc", "fmgi_kernels.hip")).read().splitlines()
     # basic blocks: targets of branches and the instruction after each branch start one
-    tgt = set()
-    back = []
-    for k, (ad, mn, ops) in enumerate(insts):
-        if mn.startswith(("s_cbranch", "s_branch")):
-            m = re.search(r"<[^>]*\+0x([0-9a-f]+)>", ops) or re.search(r"0x([0-9a-f]+)", ops)
-            # llvm-objdump prints the target as an absolute address in a comment-less operand
-            t = None
-            mt = re.search(r"(\d+)$", ops.strip())
-            if mt:
-                t = ad + 4 + 4 * int(mt.group(1)) if False else None
-            tgt.add(k + 1)
-    # targets: objdump prints "s_branch 1234" (a signed dword offset): recompute
-    for k, (ad, mn, ops) in enumerate(insts):
-        if mn.startswith(("s_cbranch", "s_branch")):
-            mt = re.search(r"(-?\d+)\s*$", ops.strip())
-            if not mt:
-                continue
-            t_addr = ad + 4 + 4 * int(mt.group(1))
-            j = next((q for q, x in enumerate(insts) if x[0] == t_addr), None)
-            if j is not None:
-                tgt.add(j)
-                if j <= k:
-                    back.append((j, k))
+    at = {x[0]: q for q, x in enumerate(insts)}
+    tgt, back = set(), []
+    for k, (ad, mn, ops, t_addr) in enumerate(insts):
+        if t_addr is None:
+            continue
+        tgt.add(k + 1)
+        j = at.get(t_addr)
+        if j is not None:
+            tgt.add(j)
+            if j <= k:
+                back.append((j, k))
     if not back:
         raise SystemExit("no loop found")
     lo, hi = max(back, key=lambda x: x[1] - x[0])
