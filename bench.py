@@ -185,16 +185,15 @@ def cpu_baseline_radiosity(target_s=10.0, procs=1):
     }
 
 
-def pmc_traffic(config_name):
-    """HBM bytes per bake launch from the committed rocprofv3 PMC summary (profiles/), if present."""
+def pmc_record(config_name):
+    """The committed rocprofv3 PMC summary of the bake (HBM bytes per launch, profiles/pmc_traffic.json)."""
     p = os.path.join(REPO, "profiles", "pmc_traffic.json")
     if not os.path.exists(p):
         return None
     try:
-        d = json.load(open(p)).get(config_name, {})
+        return json.load(open(p)).get(config_name)
     except (OSError, ValueError):
         return None
-    return d.get("hbm_bytes_per_launch") if "k_bake" in d.get("kernel", "") else None
 
 
 def sq_record(config_name):
@@ -469,10 +468,22 @@ def main():
                    "frac": atomic_rate / 2.0e10}
         # what binds the bake: counters of this config and build (profiles/sq_issue.json) against the
         # measured clock and VALU ceiling; bounded fractions only (issue_block)
+        # (only counters of the k_bake instance(s) this run launched: a summary of another instance, e.g. one
+        # taken before a kept kernel change renamed it, is reported as stale and not used)
+        instance = ctx.last_bake_kernel
         rec = sq_record(args.config)
+        pmc = pmc_record(args.config)
+        counters = {"kernel": instance,
+                    "issue_source": rec.get("source") if rec else None,
+                    "issue_matches_kernel": bool(rec) and rec.get("kernel") == instance,
+                    "traffic_source": pmc.get("source") if pmc else None,
+                    "traffic_matches_kernel": bool(pmc) and pmc.get("kernel") == instance}
         issue = issue_block(rec, ks, per_launch_scans, torch.cuda.get_device_properties(dev).multi_processor_count) \
-            if rec else None
+            if counters["issue_matches_kernel"] else None
+        traffic = pmc.get("hbm_bytes_per_launch") if counters["traffic_matches_kernel"] else None
         bound, binding = binding_of(issue, atomic_rate)
+        if rec and not counters["issue_matches_kernel"]:
+            binding = "unmeasured for this build (the committed counter summary names another kernel instance)"
         # SURVEY.md §8d FLOP roofline of the same launches: F = 40 x T + 150 x S per photon (40 = one
         # branch-free intersects(), 150 = sampling, tile index and colour per bounce), S = scans per photon,
         # T = rect tests per photon -- the tests this bake evaluates (its scans test a few records each), and
@@ -533,8 +544,9 @@ def main():
                 "peak": HBM_PEAK_GBS,
                 "unit": "GB/s",
                 "frac": achieved_gbs / HBM_PEAK_GBS,
-                "traffic": pmc_traffic(args.config),
+                "traffic": traffic,
                 "kernel": "k_bake",
+                "counters": counters,
                 "kernel_ms": bake_launch_ms,
                 "launches_per_step": bake_launches / args.steps,
                 "bake_path_ms_per_step": span_ms,

@@ -348,8 +348,8 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
    tiles (§4.1), while the fold keeps 64-KB workgroups, two per CU. */
 /* CARRY: channels summed as a u32 low word with a returning ds_add_rtn_u32 plus a u32 carry
    word that takes +-1 only when the low word wraps (old + v < old for v >= 0; a negative difference borrows
-   when old + v >= old): 0 = every channel as one ds_add_u64 (default), 1 = G - R and B - R with carries
-   (their adds wrap ~1/64 of the time), 2 = R as well. The sum mod 2^64 is the same either way: a channel is
+   when old + v >= old): 0 = every channel as one ds_add_u64, 1 = G - R and B - R with carries (their adds
+   wrap ~1/64 of the time), 2 = R as well (the default: fewer bank dwords per add, -2 % on box200's fold). The sum mod 2^64 is the same either way: a channel is
    hi * 2^32 + lo, and only hi mod 2^32 matters mod 2^64. The carry channels reuse the u64 array's 8 B per texel
    as lo[T] | hi[T]. */
 template <int EXP, int TB = FMGI_TILE_BITS, int SPLIT = 1, int CARRY = 0>
@@ -701,9 +701,12 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                            sb.tile_blocks, sb.tile_blocks + FMGI_PRESORT_MAX_TILES + 1, sb.block_list);
         typedef void (*FoldFn)(const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, int, int, int,
                                const uint4 *, unsigned long long *, int);
+        /* the channels summed as u32 low words with carry words (CARRY = 2): box200's wide fold 11.76 -> 11.54 ms,
+           bit-identical (profiles/r06/s5 ab_carry.log); the experiment build's FMGI_FOLD_CARRY=0 keeps the
+           int64 adds */
         FoldFn fn = nullptr;
-        if (split == 1 && tb == FMGI_TILE_BITS) fn = k_bucket_fold<0>;
-        else if (split == 1 && tb == 12) fn = k_bucket_fold<0, 12, 1>;
+        if (split == 1 && tb == FMGI_TILE_BITS) fn = k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
+        else if (split == 1 && tb == 12) fn = k_bucket_fold<0, 12, 1, 2>;
 #if FMGI_EXPERIMENTS
         {   /* FMGI_EXP_FOLD (profiling variants), FMGI_FOLD_SPLIT (split folds), FMGI_FOLD_CARRY (carry words) */
             const char *xe = fmgi_exp_env("FMGI_EXP_FOLD"), *ce = fmgi_exp_env("FMGI_FOLD_CARRY");
@@ -715,8 +718,8 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
             if (tb == 13 && split == 2) fn = k_bucket_fold<0, 12, 2>;
             if (tb == 13 && split == 4) fn = k_bucket_fold<0, 11, 4>;
             const bool plain = split == 1 && (tb == 12 || exp == 0);
+            if (plain && ce && carry == 0) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1> : (FoldFn)k_bucket_fold<0>;
             if (plain && carry == 1) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 1> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1>;
-            if (plain && carry == 2) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 2> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
         }
 #endif
         if (!fn) return hipErrorInvalidValue; /* no instance for this tile width and split */

@@ -740,6 +740,12 @@ struct fmgi_context {
     bool warned_cells = false;        /* the coarse LDS grid was launched unstaged (said once)          */
     /* the compact closed-box tables (fmgi_internal.h RectC ...; build_compact): set when a closed box's
        RectLds walls and 32-B cells do not fit LDS but these do; the grid is then the one they index */
+    /* the launch-tail handoff (bake_common): saved work items (16 B per lane of the saving launch) and
+       the counters {idle lanes, states saved, states resumed} */
+    uint4 *d_tail = nullptr;
+    unsigned *d_tail_ctr = nullptr;
+    uint64_t tail_cap = 0;
+    std::string last_kernel; /* fmgi_last_bake_kernel: the instance(s) the last bake launch ran */
     int grid_cpr = 0; /* fmgi_set_grid_cells_per_record: the grid's cells per record (0: the product's choice) */
     /* fmgi_set_option: the tests' handles on product paths a given scene would not take (include/flatmatch_gi.h) */
     int64_t opt[FMGI_OPT_COUNT] = {0, 0, 0, -1, -1, -1, 0, 0};
@@ -820,6 +826,8 @@ FMGI_API void fmgi_destroy(fmgi_context *c) {
     hipFree(c->d_himg);
     hipFree(c->d_himg_full);
     hipFree(c->d_blob);
+    hipFree(c->d_tail);
+    hipFree(c->d_tail_ctr);
     hipFree(c->d_grecs);
     hipFree(c->d_gidx);
     for (hipEvent_t ev : c->ev_pool) hipEventDestroy(ev);
@@ -2116,6 +2124,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
         HIPCHK(hipMemsetAsync(c->d_counter, 0, 8, s));
         hipEvent_t t0 = nullptr, t1 = nullptr;
         HIPCHK(time_begin(c, s, t0));
+        c->last_kernel = fmgi_bake_kernel_name(a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace);
         HIPCHK(fmgi_launch_bake(a, a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace,
                                 grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (e - b) * (uint64_t)a.coop,
                                             a.coop > 1 ? -1 : inst),
@@ -2154,20 +2163,39 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     }
     hipStream_t fs = overlap ? c->fold_stream : s;
     int nchunk = 0;
+    /* Experiments (FMGI_TAIL=1 / 2 / 4 in the experiment build; measured and rejected): the
+       launch tail of the layouts' hybrid scan handed to a second launch. A saving launch
+       (FMGI_KERNEL_HYBRID_TAIL) polls the launch's idle-lane count; once half of its lanes found no item left,
+       every lane still in one saves it at its next photon boundary (RNG state, photons left, source: 16 B) and
+       leaves; a resuming launch (FMGI_KERNEL_HYBRID_RESUME) finishes the saved items with FMGI_TAIL lanes each
+       splitting the wall-pair loop. Exact (the same photons, draws and hits per item), but on example.png half
+       of the lanes are idle only once 97.6 % of the scans are done, and the resuming launch (3.5 ms) costs more
+       than the tail it replaces (profiles/r06/s12). */
+    int tail_coop = 0;
+    if (const char *te = fmgi_exp_env("FMGI_TAIL")) tail_coop = atoi(te);
+    const bool tail = kernel == FMGI_KERNEL_HYBRID && inst == FMGI_KERNEL_HYBRID && !trace && a.coop == 1 &&
+                      (kacc == kAccScatter || kacc == kAccBucket) && (tail_coop == 1 || tail_coop == 2 || tail_coop == 4) &&
+                      e - b <= 16 * (uint64_t)lanes;
+    const int inst1 = tail ? FMGI_KERNEL_HYBRID_TAIL : inst;
     for (uint64_t cb = b; cb < e; cb += chunk, nchunk++) {
         const uint64_t ce = std::min(e, cb + chunk);
         const int k = overlap ? (nchunk & 1) : 0; /* one buffer set unless the folds run beside the bakes */
+        int ring_tail = 0; /* (the saving launch's LDS: the workgroup's idle-count copy before the rings) */
+        fmgi_bake_lds(inst1, kacc, block, a.fimg_bytes, &ring_tail);
         const int grid = grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, (ce - cb) * (uint64_t)a.coop,
-                                     a.coop > 1 ? -1 : inst);
+                                     a.coop > 1 ? -1 : inst1);
+        const int grid2 = tail ? grid_blocks(c, kernel, kacc, trace, block, a.fimg_bytes, UINT64_MAX, FMGI_KERNEL_HYBRID_RESUME)
+                               : 0; /* the resuming launch: every resident lane */
         /* buffer set k is free once the fold of chunk nchunk - 2 has read it (host allocation below
            happens only while growing, after a full wait) */
         if (overlap && nchunk >= 2) HIPCHK(hipStreamWaitEvent(s, c->ev_folded[k], 0));
-        if (ensure_stream_needs_growth(c, k, ce - cb, grid, block, smode)) { /* no fold may still read it */
+        /* (the pool holds one partly filled block per wave and tile: the resuming launch's waves too) */
+        if (ensure_stream_needs_growth(c, k, ce - cb, grid + grid2, block, smode)) { /* no fold may still read it */
             HIPCHK(hipStreamSynchronize(s));
             if (c->fold_stream) HIPCHK(hipStreamSynchronize(c->fold_stream));
         }
         const int tbits = tile_bits(c, smode, ce - cb);
-        int rc = ensure_stream(c, k, ce - cb, grid, block, smode, tbits);
+        int rc = ensure_stream(c, k, ce - cb, grid + grid2, block, smode, tbits);
         if (rc != FMGI_OK) return rc;
         StreamBufs &sb = c->sb[k];
         a.item_begin = cb;
@@ -2200,7 +2228,60 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
                     a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, block, grid, fmgi_bake_lds(kernel_instance(c, kernel), kacc, block, a.fimg_bytes, nullptr),
                     a.fimg_bytes, a.rects_off, a.srcs_off, a.cells_off);
         HIPCHK(time_begin(c, s, t0));
-        HIPCHK(fmgi_launch_bake(a, a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace, grid, block, s));
+        if (tail) {
+            const uint64_t lanes1 = (uint64_t)grid * (uint64_t)block;
+            if (c->tail_cap < lanes1) {
+                HIPCHK(hipStreamSynchronize(s)); /* (no earlier launch may still use the old buffers) */
+                hipFree(c->d_tail);
+                c->d_tail = nullptr;
+                c->tail_cap = 0;
+                HIPCHK(hipMalloc(&c->d_tail, lanes1 * sizeof(uint4)));
+                c->tail_cap = lanes1;
+            }
+            if (!c->d_tail_ctr) HIPCHK(hipMalloc(&c->d_tail_ctr, 4 * sizeof(unsigned)));
+            HIPCHK(hipMemsetAsync(c->d_tail_ctr, 0, 4 * sizeof(unsigned), s));
+            BakeArgs a1 = a;
+            a1.tail_idle = c->d_tail_ctr;
+            a1.tail_n = c->d_tail_ctr + 1;
+            a1.tail_next = c->d_tail_ctr + 2;
+            a1.tail_states = c->d_tail;
+            a1.tail_at = (uint32_t)(lanes1 / 2); /* half of the lanes idle */
+            if (const char *ta = fmgi_exp_env("FMGI_TAIL_AT")) /* experiments: idle lanes per mille (> 1000: never) */
+                a1.tail_at = (uint32_t)std::min<uint64_t>(lanes1 * (uint64_t)atoi(ta) / 1000, 0xFFFFFFFFull);
+            a1.ring_off = ring_tail;
+            a1.tail_flag_off = ring_tail - 16;
+            unsigned long long scans0 = 0, scans1 = 0; /* (experiments: the saving launch's share of the scans) */
+            if (fmgi_exp_env("FMGI_SHOW_TAIL")) {
+                HIPCHK(hipMemcpyAsync(&scans0, c->d_stats + KSTAT_SCANS, 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+            HIPCHK(fmgi_launch_bake(a1, FMGI_KERNEL_HYBRID_TAIL, kacc, false, grid, block, s));
+            if (fmgi_exp_env("FMGI_SHOW_TAIL")) {
+                HIPCHK(hipMemcpyAsync(&scans1, c->d_stats + KSTAT_SCANS, 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+            }
+            BakeArgs a2 = a1;
+            a2.tail_at = 0;
+            a2.coop = tail_coop;
+            a2.fetch_tab = nullptr;
+            a2.fetch_nseg = 0;
+            fmgi_bake_lds(FMGI_KERNEL_HYBRID_RESUME, kacc, block, a.fimg_bytes, &a2.ring_off);
+            HIPCHK(fmgi_launch_bake(a2, FMGI_KERNEL_HYBRID_RESUME, kacc, false, grid2, block, s));
+            c->last_kernel = fmgi_bake_kernel_name(FMGI_KERNEL_HYBRID_TAIL, kacc, false) + " + " +
+                             fmgi_bake_kernel_name(FMGI_KERNEL_HYBRID_RESUME, kacc, false);
+            if (fmgi_exp_env("FMGI_SHOW_TAIL")) { /* experiments: idle lanes, states saved, states resumed */
+                unsigned h[4] = {0, 0, 0, 0};
+                unsigned long long scans2 = 0;
+                HIPCHK(hipMemcpyAsync(h, c->d_tail_ctr, sizeof h, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipMemcpyAsync(&scans2, c->d_stats + KSTAT_SCANS, 8, hipMemcpyDeviceToHost, s));
+                HIPCHK(hipStreamSynchronize(s));
+                fprintf(stderr, "fmgi: tail lanes %llu grid2 %d idle %u saved %u resumed %u scans %llu + %llu\n",
+                        (unsigned long long)lanes1, grid2, h[0], h[1], h[2], scans1 - scans0, scans2 - scans1);
+            }
+        } else {
+            c->last_kernel = fmgi_bake_kernel_name(a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace);
+            HIPCHK(fmgi_launch_bake(a, a.coop > 1 ? kernel_instance(c, kernel) : inst, kacc, trace, grid, block, s));
+        }
         HIPCHK(time_end(c, s, t0, t1, c->ev_bake));
         if (overlap) {
             HIPCHK(hipEventRecord(c->ev_baked[k], s));
@@ -2219,6 +2300,17 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
 }
 
 FMGI_API int fmgi_auto_kernel(const fmgi_context *c) { return c ? c->auto_kernel : FMGI_ERR_ARG; }
+
+FMGI_API int fmgi_last_bake_kernel(const fmgi_context *c, char *buf, int cap) {
+    if (!c || (cap > 0 && !buf) || cap < 0) return set_err(FMGI_ERR_ARG, "fmgi_last_bake_kernel: bad arguments");
+    const int n = (int)c->last_kernel.size();
+    if (cap > 0) {
+        const int k = n < cap - 1 ? n : cap - 1;
+        memcpy(buf, c->last_kernel.data(), (size_t)k);
+        buf[k] = 0;
+    }
+    return n;
+}
 
 FMGI_API int fmgi_set_timing(fmgi_context *c, int on) {
     if (!c) return set_err(FMGI_ERR_ARG, "null context");

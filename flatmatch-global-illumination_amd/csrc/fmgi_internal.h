@@ -8,6 +8,8 @@
 #include <hip/hip_runtime_api.h>
 #include <stdint.h>
 
+#include <string>
+
 #include "fmgi_lds_attr.h"
 
 #include "fmgi_core.h"
@@ -165,6 +167,15 @@ struct BakeArgs {
     /* the compact closed-box instance (FMGI_KVAR_COMPACT): byte offsets in the staged blob of the RectC,
        ClassC, filter-extent (float4 by rect index) and CellC tables, and the dummy record's index */
     int rectc_off, class_off, recf_off, cellc_off, cdummy;
+    /* the launch tail of layouts with few work items per lane (ScanHybridT's Tail modes, fmgi_api.cpp
+       bake_common): the saving launch counts its lanes that found no item left in *tail_idle and, once
+       tail_at of them are idle, every lane still in an item saves it at its next photon boundary (tail_states[*tail_n++], 16 B)
+       and leaves; the resuming launch's groups of `coop` lanes take the saved states through *tail_next and
+       finish those items with the wall loop split among them */
+    unsigned *tail_idle, *tail_n, *tail_next;
+    uint32_t tail_at;
+    int tail_flag_off;    /* the saving launch: LDS byte offset of the workgroup's copy of *tail_idle */
+    uint4 *tail_states;
     int coop;             /* lanes per work item (1, 2, 4, 8; ScanFast only): small launches split each
                              scan's records over several lanes instead of leaving the GPU mostly idle */
     /* AccState accumulation: u64 counts[FMGI_COLOUR_STATES][num_texels] */
@@ -269,6 +280,9 @@ int fmgi_fold_split(int tile_bits); /* fold tiles per bucket tile of 2^tile_bits
 
 /* internal kernel id (not in the C ABI): ScanFast with BakeArgs::coop lanes per work item */
 #define FMGI_KERNEL_FAST_COOP 101
+/* internal kernel ids of the launch-tail handoff (FMGI_KERNEL_HYBRID): the saving and the resuming launch */
+#define FMGI_KERNEL_HYBRID_TAIL 102
+#define FMGI_KERNEL_HYBRID_RESUME 103
 
 /* accum: 1 = AccFx3, 2 = AccState, 3 = AccNone (profiling only), 4 = AccStream (unsorted / presorted
    stream layouts), kAccBucket = AccBucket (the stream in the per-tile bucket layout, BakeArgs::presort 2:
@@ -291,6 +305,8 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
                             hipStream_t s);
 int fmgi_bake_resident_blocks(int kernel, int accum, bool trace, int block, int lds_bytes);
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off);
+/* the profiler's name of the k_bake instance (kernel, accum, trace) runs (fmgi_last_bake_kernel) */
+std::string fmgi_bake_kernel_name(int kernel, int accum, bool trace);
 int fmgi_kernels_filter_pk(); /* the kernels' FMGI_FILTER_PK (whether the hybrid scan reads the pair image) */
 hipError_t fmgi_launch_reduce_states(unsigned long long *counts, const long long *colfx, unsigned long long *lm,
                                      int n, hipStream_t s);

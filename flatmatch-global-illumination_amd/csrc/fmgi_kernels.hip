@@ -18,8 +18,10 @@
  */
 #include <hip/hip_runtime.h>
 
+#include <cxxabi.h>
 #include <mutex>
 #include <set>
+#include <string>
 #include <utility>
 
 #include "fmgi_internal.h"
@@ -347,7 +349,7 @@ __device__ __forceinline__ void pair_rec(float f, float uu, float vv, float hu, 
 }
 
 template <int A>
-__device__ __forceinline__ void filter_pairs(const char *img, int G, f3 s, f3 d, float &L1, float &L2,
+__device__ __forceinline__ void filter_pairs(const char *img, int g0, int G, f3 s, f3 d, float &L1, float &L2,
                                              int &code1) {
     constexpr int U = (A == 0) ? 1 : 0;
     constexpr int V = (A == 2) ? 1 : 2;
@@ -369,7 +371,7 @@ __device__ __forceinline__ void filter_pairs(const char *img, int G, f3 s, f3 d,
     /* two groups per iteration with all six reads issued first (left to itself, the scheduler waits
        for each group's reads right after issuing them, exposing the LDS latency once per group;
        example.png bake 21.07 -> 20.78 ms, profiles/r05/s20) */
-    int g = 0;
+    int g = g0;
     for (; g + 1 < G; g += 2) {
         const float4 a0 = p[6 * g], a1 = p[6 * g + 1], a2 = p[6 * g + 2];
         const float4 b0 = p[6 * g + 6], b1 = p[6 * g + 7], b2 = p[6 * g + 8];
@@ -381,7 +383,7 @@ __device__ __forceinline__ void filter_pairs(const char *img, int G, f3 s, f3 d,
     if (g < G) group(p[6 * g], p[6 * g + 1], p[6 * g + 2]);
 #else
 #pragma unroll 2
-    for (int g = 0; g < G; g++) group(p[6 * g], p[6 * g + 1], p[6 * g + 2]);
+    for (int g = g0; g < G; g++) group(p[6 * g], p[6 * g + 1], p[6 * g + 2]);
 #endif
 }
 
@@ -1044,33 +1046,45 @@ __device__ __forceinline__ void plan_walls(const BakeArgs &a, const char *img, f
  * candidate sets and the keys are theirs, so phase 2, the separation test and the fallback are
  * ScanFast's. Grid candidates carry the rect index with the 0x40000000 flag (BakeArgs::grid_code_or).
  */
-template <bool Plan>
+/* Tail (the launch-tail handoff, BakeArgs::tail_*): 0 = the plain instance; 1 = the saving launch (k_bake hands
+   its lanes' items off once enough lanes are idle); 2 = the resuming launch, whose groups of BakeArgs::coop lanes
+   hold the same photon state and split the wall-pair loop (the floors' grid walk on the group's first lane, so
+   every record is tested by exactly one lane and coop_merge's L2 stays the true runner-up) */
+template <bool Plan, int Tail = 0>
 struct ScanHybridT {
+    static_assert(!Plan || Tail == 0, "the floor-plan walk has no tail instances");
     static constexpr bool kLds = true;
-    static constexpr bool kCoop = false;
+    static constexpr bool kCoop = Tail == 2;
+    static constexpr int kTail = Tail;
     static constexpr int kMinWaves = 1; /* k_bake occupancy floor for the register allocator */
     static __device__ __forceinline__ void scan(const BakeArgs &a, const char *lds, f3 src, f3 dir, HitRec &h,
                                                 ScanStats &st) {
         float L1 = INFINITY, L2 = INFINITY;
         int code1 = -1;
         unsigned ntest = 0;
-        grid_axis<2>(a, lds + uni(a.hyb_off), 128 * (uni(a.gJ[0]) + uni(a.gJ[1])), uni(a.gJ[2]), src, dir, L1, L2,
-                     code1, ntest);
+        const int coop = kCoop ? a.coop : 1, sub = kCoop ? (int)__lane_id() & (coop - 1) : 0;
+        if (!kCoop || sub == 0)
+            grid_axis<2>(a, lds + uni(a.hyb_off), 128 * (uni(a.gJ[0]) + uni(a.gJ[1])), uni(a.gJ[2]), src, dir, L1,
+                         L2, code1, ntest);
         if (Plan) { /* the walls the ray's floor-plan cells list, nearest cells first, after the floors */
             plan_walls(a, lds, src, dir, L1, L2, code1, ntest);
         } else {
 #if FMGI_FILTER_PK
-            /* the walls: the pair image, two records per packed iteration; codes are rect indices */
-            filter_pairs<0>(lds + uni(a.pair_off), uni(a.pG[0]), src, dir, L1, L2, code1);
-            filter_pairs<1>(lds + uni(a.pair_off) + 96 * uni(a.pG[0]), uni(a.pG[1]), src, dir, L1, L2, code1);
+            /* the walls: the pair image, two records per packed iteration; codes are rect indices (coop lanes:
+               sub-lane `sub` takes groups [sub T, sub T + T) of each axis) */
+            const int G0 = uni(a.pG[0]), G1 = uni(a.pG[1]);
+            const int T0 = kCoop ? (G0 + coop - 1) / coop : G0, T1 = kCoop ? (G1 + coop - 1) / coop : G1;
+            const int s0 = sub * T0, s1 = sub * T1;
+            filter_pairs<0>(lds + uni(a.pair_off), s0, s0 + T0 < G0 ? s0 + T0 : G0, src, dir, L1, L2, code1);
+            filter_pairs<1>(lds + uni(a.pair_off) + 96 * G0, s1, s1 + T1 < G1 ? s1 + T1 : G1, src, dir, L1, L2, code1);
 #else       /* experiments (FMGI_FILTER_PK=0 builds): one record per iteration over the filter image */
-            filter_axis<0, false>(lds, a.fJ[0], 0, 1, src, dir, L1, L2, code1);
-            filter_axis<1, false>(lds + 64 * a.fJ[0], a.fJ[1], 0, 1, src, dir, L1, L2, code1);
+            filter_axis<0, kCoop>(lds, a.fJ[0], sub, coop, src, dir, L1, L2, code1);
+            filter_axis<1, kCoop>(lds + 64 * a.fJ[0], a.fJ[1], sub, coop, src, dir, L1, L2, code1);
 #endif
             ntest += (unsigned)(a.fJ[0] + a.fJ[1]);
         }
         cptr<int32_t> G = (cptr<int32_t>)a.general;
-        for (int g = 0; g < uni(a.ngeneral); g++) { /* not axis-aligned: exact order-independent tests */
+        for (int g = sub; g < uni(a.ngeneral); g += coop) { /* not axis-aligned: exact order-independent tests */
             const float f = exact_on_v(a.rects, G[g], src, dir, INFINITY);
             const float key = (f < 0) ? INFINITY : f;
             const bool lt = key < L1;
@@ -1078,6 +1092,7 @@ struct ScanHybridT {
             code1 = lt ? (0x20000000 | g) : code1;
             L1 = lt ? key : L1;
         }
+        if (kCoop) coop_merge(coop, L1, L2, code1);
         st.tests += ntest + (uint32_t)a.ngeneral;
         if (L1 == INFINITY) {
             h.best = INFINITY;
@@ -1113,6 +1128,8 @@ struct ScanHybridT {
 
 using ScanHybrid = ScanHybridT<false>;
 using ScanHybridPlan = ScanHybridT<true>;
+using ScanHybridTail = ScanHybridT<false, 1>;
+using ScanHybridResume = ScanHybridT<false, 2>;
 
 /* ---- accumulation policies -------------------------------------------------------------------- */
 
@@ -2045,6 +2062,68 @@ __device__ __forceinline__ SrcDev src_fields(const R &r) {
     return d;
 }
 
+/* whether a scan's lanes fetch work items with one atomic per wave (wave_ticket64) rather than one per lane:
+   the hybrid scan's launches of a few costly items per lane, +1-2 % on example.png (every lane fetches at
+   the launch's start); the grid scans' launches of dozens of items per lane lose 0.1-0.3 % (box200) and
+   1 % (box2000) with it (profiles/r06/s14) */
+template <class Scan, class = void>
+struct ScanFetchAgg {
+    static constexpr bool value = false;
+};
+template <class Scan>
+struct ScanFetchAgg<Scan, decltype((void)Scan::kTail)> {
+    static constexpr bool value = true;
+};
+
+/* the launch-tail mode of a scan instance (ScanHybridT::kTail: 1 saving, 2 resuming), else 0 */
+template <class Scan, class = void>
+struct ScanTail {
+    static constexpr int value = 0;
+};
+template <class Scan>
+struct ScanTail<Scan, decltype((void)Scan::kTail)> {
+    static constexpr int value = Scan::kTail;
+};
+
+/* a work item in flight as the launch-tail handoff saves it, at a photon boundary (16 B): between two photons
+   the position, direction, colour, sample basis, depth and colour state are all dead (the next photon's
+   emission sets them), so the item's RNG state, its photons left and its source are the whole state.
+   (The item's index and photon number serve the trace kernels only, which have no tail launches.) */
+__device__ __forceinline__ void tail_save(uint4 *d, uint32_t rng, int left, int srci, uint32_t scans) {
+    *d = make_uint4(rng, (uint32_t)left, (uint32_t)srci, scans);
+}
+__device__ __forceinline__ void tail_load(const uint4 *d, uint32_t &rng, int &left, int &srci, uint32_t &scans) {
+    const uint4 q = *d;
+    rng = q.x;
+    left = (int)q.y;
+    srci = (int)q.z;
+    scans = q.w;
+}
+
+/* wave_ticket on a 64-bit counter (the work-item queue) */
+__device__ __forceinline__ uint64_t wave_ticket64(unsigned long long *ctr, bool on) {
+    const uint64_t m = __ballot(on);
+    const int leader = __ffsll((long long)m) - 1;
+    uint64_t base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(ctr, (unsigned long long)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
+/* one device-scope atomicAdd for every lane of the wave that has `on` set (they must all be active here):
+   returns each such lane's value old + its rank among them. Many lanes reaching a counter at once (the
+   launch-tail saves and resumes) otherwise queue on its one word at the L2's rate for a single address
+   (MI355X_MICROARCH.md, dequeue: ~88 per us): 190k saves cost the saving launch 2 ms */
+__device__ __forceinline__ uint32_t wave_ticket(unsigned *ctr, bool on) {
+    const uint64_t m = __ballot(on);
+    if (!m) return 0u;
+    const int leader = __ffsll((long long)m) - 1;
+    uint32_t base = 0;
+    if ((int)__lane_id() == leader) base = atomicAdd(ctr, (unsigned)__popcll(m));
+    base = __shfl(base, leader, 64);
+    return base + __builtin_amdgcn_mbcnt_hi((uint32_t)(m >> 32), __builtin_amdgcn_mbcnt_lo((uint32_t)m, 0u));
+}
+
 /* whether a scan's instance compiles the tables' global paths out (ScanGridT::kStaged) */
 template <class Scan, class = void>
 struct ScanStaged {
@@ -2118,6 +2197,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     if (Scan::kLds) { /* stage the filter image once per workgroup */
         const int n16 = a.fimg_bytes >> 4;
         for (int i = threadIdx.x; i < n16; i += blockDim.x) ((uint4 *)s_img)[i] = ((const uint4 *)a.fimg)[i];
+        if (ScanTail<Scan>::value == 1 && threadIdx.x == 0) *(uint32_t *)(s_img + a.tail_flag_off) = 0u;
         __syncthreads();
     }
     if constexpr (HasAppend<Acc>::value)
@@ -2132,6 +2212,11 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
     /* per-lane counts of one launch, in 32 bits: a lane traces a few dozen work items per launch (the
        grid is occupancy-sized, chunks are memory-sized); scans = deposits + escapes */
     uint32_t n_ph = 0, n_dep = 0, n_esc = 0;
+#ifdef FMGI_NO_LANE_STATS /* PROFILING ONLY: the deposit / escape counters compiled out (their registers' cost) */
+#define FMGI_LANE_COUNT(x) ((void)0)
+#else
+#define FMGI_LANE_COUNT(x) (x)
+#endif
     ScanStats sst;
     WaveStream ws;
     /* BakeArgs::coop lanes per work item (ScanFast splits each scan's records among them; they keep
@@ -2142,11 +2227,33 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
 #ifdef FMGI_CLOCK_STAMP /* diagnostic build: the in-kernel clock (MI355X_MICROARCH.md, DVFS item 6) */
     const unsigned long long ck_t0 = __builtin_amdgcn_s_memtime(), ck_r0 = __builtin_amdgcn_s_memrealtime();
 #endif
+    constexpr int kTail = ScanTail<Scan>::value;
+    bool tail_saving = false; /* (the saving launch) this lane left the loop to hand its item off */
+    uint32_t tail_it = 0;      /* (the saving launch) the wave's iterations, for its turn to poll */
+    /* (the resuming launch) the items the saving launch saved: final before this launch started */
+    const uint32_t tail_saved = kTail == 2 ? *a.tail_n : 0u;
     for (;;) {
+        if constexpr (kTail == 2) {
+            /* the resuming launch: a group's lanes take the next saved item instead of a new one (the wave's
+               groups that need one take consecutive tickets with one atomic) */
+            if (start && left == 0) {
+                if (uni(a.src_cost) && lead && photon >= 0)
+                    atomicAdd(a.src_cost + srci, (unsigned long long)(n_dep + n_esc));
+                uint32_t w = wave_ticket(a.tail_next, lead);
+                w = __shfl(w, (int)__lane_id() & ~(a.coop - 1), 64);
+                if (w >= tail_saved) break;
+                uint32_t done = 0; /* the item's scans in the saving launch */
+                tail_load(a.tail_states + w, rng, left, srci, done);
+                win = srci < a.nwindows;
+                photon = 0; /* (an item in flight: >= 0 for the per-source scan totals) */
+                if (uni(a.src_cost) && lead)
+                    atomicAdd(a.src_cost + srci, (unsigned long long)done - (unsigned long long)(n_dep + n_esc));
+            }
+        }
         /* ---- stage 1: new photon (and new work item), then the iteration's one direction sample ---- */
         float edx = 0, edy = 0;
         if (start) {
-            if (left == 0) {
+            if (kTail != 2 && left == 0) {
                 if (TRACE && photon >= 0) {
                     a.ev_counts[item - a.item_begin] = nev;
                     a.rng_final[item - a.item_begin] = rng;
@@ -2160,10 +2267,18 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
                     atomicAdd(a.stats + KSTAT_TESTS, (unsigned long long)sst.tests);
                 }
                 sst.tests = 0;
-                /* one fetch per work item: by the group's lead lane, broadcast to its coop lanes */
-                uint64_t w = lead ? atomicAdd(a.counter, 1ull) : 0ull;
+                /* one fetch per work item: by the group's lead lane, broadcast to its coop lanes (the hybrid
+                   scan: the wave's leads that fetch in the same iteration take consecutive items with one
+                   atomic, ScanFetchAgg) */
+                uint64_t w = ScanFetchAgg<Scan>::value ? wave_ticket64(a.counter, lead) : (lead ? atomicAdd(a.counter, 1ull) : 0ull);
                 if (Scan::kCoop) w = __shfl(w, (int)__lane_id() & ~(a.coop - 1), 64);
-                if (w >= a.item_end - a.item_begin) break;
+                if (w >= a.item_end - a.item_begin) {
+                    if constexpr (kTail == 1) { /* more lanes without work: one atomic per wave */
+                        const uint64_t m = __ballot(true);
+                        if ((int)__lane_id() == __ffsll((long long)m) - 1) atomicAdd(a.tail_idle, (unsigned)__popcll(m));
+                    }
+                    break;
+                }
                 if (uni(a.fetch_nseg) > 0) { /* fetch order: segments of source ranges, costliest items first
                                            (32-bit: the host builds a table only below 2^32 items) */
                     const uint32_t f = (uint32_t)w;
@@ -2231,7 +2346,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         sbv = mkf3(h.bvx, h.bvy, h.bvz);
         if (h.best == INFINITY) { /* photonmap.cl:208-209 */
             start = true;
-            n_esc++;
+            FMGI_LANE_COUNT(n_esc++);
         } else {
         /* ---- stage 3: hit (photonmap.cl:216-258) ---- */
         pos = add3(pos, mul3(dir, h.best));
@@ -2259,7 +2374,7 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         if (lead) Acc::deposit(a, texel, sid, col);
         dep = true;
         code = ((uint32_t)texel << 10) | (uint32_t)sid;
-        n_dep++;
+        FMGI_LANE_COUNT(n_dep++);
         if (TRACE) {
             EventDev e;
             e.photon = photon;
@@ -2279,6 +2394,21 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         sst.clk.lap(ST_HIT);
         if constexpr (HasAppend<Acc>::value) Acc::append(a, ws, ring, dep && lead, code);
         sst.clk.lap(ST_APPEND);
+        if constexpr (kTail == 1) {
+            /* the launch tail: once tail_at lanes of the launch found no work item left, a lane whose photon just
+               ended saves its item for the resuming launch and leaves (a lane between items fetches at the next
+               iteration: none left, so it goes idle). The workgroup reads the idle count from its LDS copy,
+               which each wave refreshes from the global counter once in 64 of its iterations, the waves of a
+               workgroup in turn: a poll is a vector load, and its wait on gfx950 also waits for the wave's
+               scattered deposit stores (a poll per photon start cost the loop a fifth of its speed) */
+            uint32_t *seen = (uint32_t *)(s_img + a.tail_flag_off);
+            if (((tail_it++ + 8u * (threadIdx.x >> 6)) & 63u) == 0u)
+                *(volatile uint32_t *)seen = __hip_atomic_load(a.tail_idle, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            if (start && left > 0 && *(volatile uint32_t *)seen >= uni(a.tail_at)) {
+                tail_saving = true; /* (saved after the loop) */
+                break;
+            }
+        }
     }
 #ifdef FMGI_CLOCK_STAMP /* sum over waves of the shader-clock and 100-MHz deltas of the loop: stats[24], [25] */
     {
@@ -2289,6 +2419,11 @@ __global__ __launch_bounds__(1024) FMGI_BAKE_ATTR void k_bake(BakeArgs a) {
         }
     }
 #endif
+    if constexpr (kTail == 1) { /* (every lane of the wave is here) the saving lanes' tickets, one atomic per wave */
+        const uint32_t k = wave_ticket(a.tail_n, tail_saving);
+        if (tail_saving) /* (its scans so far go to the source's total with the resuming launch's atomic) */
+            tail_save(a.tail_states + k, rng, left, srci, uni(a.src_cost) && photon >= 0 ? n_dep + n_esc : 0u);
+    }
     if constexpr (HasAppend<Acc>::value) Acc::finish(a, ws, ring);
     if (TRACE && photon >= 0) {
         a.ev_counts[item - a.item_begin] = nev;
@@ -2528,6 +2663,16 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
                : accum == 4 ? kernel_ptr<ScanFastCoop, AccStream>(false)
 #endif
                                     : nullptr;
+#if FMGI_EXPERIMENTS
+    if (kernel == FMGI_KERNEL_HYBRID_TAIL) /* the launch-tail pair: lane-by-lane stores and the rings */
+        return accum == kAccScatter ? kernel_ptr<ScanHybridTail, AccScatter>(false)
+               : accum == kAccBucket ? kernel_ptr<ScanHybridTail, AccBucket>(false) : nullptr;
+    if (kernel == FMGI_KERNEL_HYBRID_RESUME)
+        return accum == kAccScatter ? kernel_ptr<ScanHybridResume, AccScatter>(false)
+               : accum == kAccBucket ? kernel_ptr<ScanHybridResume, AccBucket>(false) : nullptr;
+#else
+    if (kernel == FMGI_KERNEL_HYBRID_TAIL || kernel == FMGI_KERNEL_HYBRID_RESUME) return nullptr;
+#endif
     if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_COMPACT)) /* the lane-by-lane stores only (bake_common) */
         return accum == kAccScatter ? kernel_ptr<ScanGridAxesCompact, AccScatter>(trace) : nullptr;
     if (kernel == (2 | FMGI_KVAR_AXES | FMGI_KVAR_STAGED)) return kernel_acc<ScanGridAxesStaged>(accum, trace);
@@ -2549,7 +2694,8 @@ const void *bake_kernel(int kernel, int accum, bool trace) {
 int fmgi_kernels_filter_pk() { return FMGI_FILTER_PK; }
 
 size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_off) {
-    const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) : 0;
+    /* (the launch-tail saving instance: the workgroup's copy of the idle-lane count after the image) */
+    const size_t img = kernel != 0 ? (((size_t)img_bytes + 15) & ~(size_t)15) + (kernel == FMGI_KERNEL_HYBRID_TAIL ? 16 : 0) : 0;
     if (ring_off) *ring_off = (int)img;
 #if FMGI_EXPERIMENTS
     if (accum == kAccLines) return img + (size_t)FMGI_LINES_DWORDS * 4;
@@ -2557,6 +2703,20 @@ size_t fmgi_bake_lds(int kernel, int accum, int block, int img_bytes, int *ring_
     if (accum == kAccScatter) return img + (size_t)(block / 64) * FMGI_SCATTER_STRIDE * 4;
     if (accum == kAccBucket) return img + (size_t)(block / 64) * FMGI_RING_STRIDE_BUCKET * 4;
     return img + ((accum == 4 || accum == kAccSliced) ? (size_t)(block / 64) * FMGI_RING_STRIDE * 4 : 0);
+}
+
+/* the name a profiler prints for the k_bake instance a launch of (kernel, accum, trace) runs ("void (anonymous
+   namespace)::k_bake<...>(BakeArgs)", as in rocprofv3's kernel trace and the committed counter summaries):
+   the runtime's symbol name of the instance, demangled; "" if there is none */
+std::string fmgi_bake_kernel_name(int kernel, int accum, bool trace) {
+    const void *fn = bake_kernel(kernel, accum, trace);
+    const char *m = fn ? hipKernelNameRefByPtr(fn, nullptr) : nullptr;
+    if (!m) return std::string();
+    int st = 0;
+    char *d = abi::__cxa_demangle(m, nullptr, nullptr, &st);
+    std::string n = st == 0 && d ? std::string(d) : std::string(m);
+    free(d);
+    return n;
 }
 
 /* a bake launch of more than 64 KiB of dynamic LDS (scan image + staged tables + rings, fmgi_api.cpp
@@ -2607,6 +2767,14 @@ hipError_t fmgi_launch_bake(const BakeArgs &a, int kernel, int accum, bool trace
         else launch3<ScanFastCoop, AccStream>(a, false, grid, blk, lds, s);
     } else if (kernel == (4 | FMGI_KVAR_PLAN)) { /* FMGI_KERNEL_HYBRID, walls over the floor plan */
         ok = launch_acc<ScanHybridPlan>(a, accum, trace, grid, blk, lds, s);
+#endif
+#if FMGI_EXPERIMENTS
+    } else if (kernel == FMGI_KERNEL_HYBRID_TAIL || kernel == FMGI_KERNEL_HYBRID_RESUME) { /* the launch tail */
+        if (trace || !bake_kernel(kernel, accum, false)) return hipErrorInvalidValue;
+        if (kernel == FMGI_KERNEL_HYBRID_TAIL && accum == kAccScatter) launch3<ScanHybridTail, AccScatter>(a, false, grid, blk, lds, s);
+        else if (kernel == FMGI_KERNEL_HYBRID_TAIL) launch3<ScanHybridTail, AccBucket>(a, false, grid, blk, lds, s);
+        else if (accum == kAccScatter) launch3<ScanHybridResume, AccScatter>(a, false, grid, blk, lds, s);
+        else launch3<ScanHybridResume, AccBucket>(a, false, grid, blk, lds, s);
 #endif
     } else if (kernel == 4) { /* FMGI_KERNEL_HYBRID */
         ok = launch_acc<ScanHybrid>(a, accum, trace, grid, blk, lds, s);

@@ -184,6 +184,16 @@ class Context:
     def auto_kernel(self) -> int:
         return int(self.lib.fmgi_auto_kernel(self.h))
 
+    @property
+    def last_bake_kernel(self) -> str:
+        """the profiler's name of the k_bake instance(s) the last bake launch ran (fmgi_last_bake_kernel)"""
+        if not hasattr(self.lib, "fmgi_last_bake_kernel"):  # (FMGI_LIB=base: an A/B build that predates it)
+            return ""
+        n = int(self.lib.fmgi_last_bake_kernel(self.h, None, 0))
+        buf = C.create_string_buffer(n + 1)
+        self.lib.fmgi_last_bake_kernel(self.h, buf, n + 1)
+        return buf.value.decode()
+
     def set_timing(self, on: bool = True):
         check(self.lib.fmgi_set_timing(self.h, 1 if on else 0), "fmgi_set_timing")
 

@@ -244,6 +244,11 @@ int fmgi_finalize(fmgi_context *ctx, const void *lm_fx_dev, const void *texels_i
                   void *stream);
 /* The kernel FMGI_KERNEL_AUTO resolves to for the current scene. */
 int fmgi_auto_kernel(const fmgi_context *ctx);
+/* The profiler's name of the k_bake instance the last bake launch ran ("void (anonymous namespace)::k_bake<...>
+   (BakeArgs)"; two names joined by " + " for the launch-tail pair), written NUL-terminated into buf (truncated
+   to cap - 1 characters); returns its full length, 0 before the first bake. No reference counterpart: the
+   measurement's handle on which instance the committed counter summaries must name. */
+int fmgi_last_bake_kernel(const fmgi_context *ctx, char *buf, int cap);
 /* Device-side timing of the bake's kernels (HIP events around each launch, on the bake's stream), off
    by default. fmgi_get_timing synchronises, returns the sums since the previous call and resets them. */
 typedef struct {

@@ -161,7 +161,8 @@ def test_no_gpu_fails_loudly(tmp_path):
     assert "[Err] performGlobalIlluminationCl" in r.stdout and "UNREACHABLE" not in r.stdout
 
 
-@pytest.mark.parametrize("items,ngpu,nshard", [(100_000_256, 8, 8), (1_001_216, 4, 4), (17, 2, 3), (5, 8, 8),
+@pytest.mark.parametrize("items,ngpu,nshard", [(100_000_256, 8, 8), (10_000_128, 8, 8), (10_000_128, 8, 16),
+                                                (1_001_216, 8, 8), (1_001_216, 4, 4), (17, 2, 3), (5, 8, 8),
                                                 (391 * 25_600, 3, 7), (0, 2, 2)])
 def test_dropin_shard_layout_and_reduction_tree(items, ngpu, nshard):
     """The drop-in's multi-GPU plan (used by bake_geometry_devices): shards partition the work items in

@@ -94,6 +94,16 @@ def test_config2_full_lightmap_exact(torch_cuda, example_scene, offsets):
     # (3 items per lane: the reordered fetch table is in use) and must give the same bits
     lm2 = _bake_gpu(torch_cuda, ctx, 0, n)
     assert np.array_equal(lm2, lm)
+    assert "ScanHybridT<false, 0>" in ctx.last_bake_kernel, ctx.last_bake_kernel
+    if fmgi.experiments():  # the rejected launch-tail handoff: the same bits
+        for coop in ("2", "1"):
+            os.environ["FMGI_TAIL"] = coop
+            try:
+                lm3 = _bake_gpu(torch_cuda, ctx, 0, n)
+            finally:
+                del os.environ["FMGI_TAIL"]
+            assert "ScanHybridT<false, 1>" in ctx.last_bake_kernel and "ScanHybridT<false, 2>" in ctx.last_bake_kernel
+            assert np.array_equal(lm3, lm)
     ctx.close()
 
 

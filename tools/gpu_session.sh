@@ -24,6 +24,10 @@
 #   grbm / tcp / sq3 one --pmc pass each: GRBM clock + SQ cycle split / TA-TD-TCP (vector memory path) / SQ memory issue
 #   rehearse         bench.py's N-rank path with REHEARSE_N (default 2) gloo ranks sharing the box's one GPU
 #   clock            bench with the in-kernel clock build (make -C <pkg> variant VNAME=clock VFLAGS=-DFMGI_CLOCK_STAMP)
+#   counters         per config in $COUNTER_CONFIGS (default box200 example box2000), into $OUT/<config>/: the bench
+#                    line (bench_<config>.log in $OUT), kernel trace, FETCH/WRITE, SQ, GRBM, TA/TD/TCP passes and the
+#                    clock build; then tools/{timed_launches,sq_summary,pmc_summary}.py over them (the summaries are
+#                    written to $OUT/sq_issue.json and $OUT/pmc_traffic.json; copy them to profiles/ after review)
 # Each GPU step has its own time limit; a crash/timeout (rc > 1) stops the session.
 set -u
 cd "$(dirname "$0")/.."
@@ -77,6 +81,23 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
     sq3)   step sq3 600 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA -d "$OUT/sq3" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
     rehearse) step rehearse 600 env FMGI_BENCH_BACKEND=gloo python -m torch.distributed.run --nnodes=1 --nproc-per-node ${REHEARSE_N:-2} --master-addr 127.0.0.1 --master-port 29517 bench.py --gpus ${REHEARSE_N:-2} --steps 3 --warmup 1 --no-cpu-baseline ;;
     clock) step clock 600 env FMGI_LIB=clock python bench.py --steps 5 --warmup 3 --no-cpu-baseline ${PROF_ARGS:-} ;;
+    counters) for cfg in ${COUNTER_CONFIGS:-box200 example box2000}; do
+               C=(--config "$cfg"); D="$OUT/$cfg"; mkdir -p "$D"
+               step "bench_$cfg" 600 python bench.py --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/prof" 600 rocprofv3 --kernel-trace --stats -d "$D/prof" -o run --output-format csv -- python bench.py --steps 3 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/pmc_fetch" 600 rocprofv3 --pmc FETCH_SIZE -d "$D/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/pmc_write" 600 rocprofv3 --pmc WRITE_SIZE -d "$D/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/sq1" 600 rocprofv3 --pmc SQ_WAVE_CYCLES SQ_ACTIVE_INST_ANY SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU SQ_INSTS_VMEM_RD SQ_INSTS_SALU -d "$D/sq1" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/sq2" 600 rocprofv3 --pmc SQ_INSTS_VALU_FLOPS_FP64 SQ_INSTS_VALU_TRANS_F32 SQ_INSTS_VALU_INT32 SQ_THREAD_CYCLES_VALU SQ_INSTS_LDS SQ_BUSY_CYCLES SQ_WAVES SQ_INSTS_BRANCH -d "$D/sq2" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/sq3" 600 rocprofv3 --pmc SQ_INSTS_VMEM SQ_INSTS_SMEM SQ_ACTIVE_INST_VMEM SQ_INST_LEVEL_VMEM SQ_WAIT_INST_ANY SQ_ACTIVE_INST_LDS SQ_WAVE_CYCLES SQ_ACTIVE_INST_SCA -d "$D/sq3" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/grbm" 600 rocprofv3 --pmc GRBM_GUI_ACTIVE GRBM_COUNT SQ_WAVE_CYCLES SQ_BUSY_CYCLES SQ_WAVES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY -d "$D/grbm" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/tcp" 600 rocprofv3 --pmc TA_TA_BUSY_sum TA_ADDR_STALLED_BY_TC_CYCLES_sum TD_TD_BUSY_sum TD_TC_STALL_sum TCP_TOTAL_CACHE_ACCESSES_sum TCP_PENDING_STALL_CYCLES_sum TCP_TCP_TA_DATA_STALL_CYCLES_sum TCP_READ_TAGCONFLICT_STALL_CYCLES_sum GRBM_GUI_ACTIVE -d "$D/tcp" -o run --output-format csv -- python bench.py --steps 1 --warmup 1 --no-cpu-baseline "${C[@]}" &&
+               step "$cfg/clock" 600 env FMGI_LIB=clock python bench.py --steps 5 --warmup 3 --no-cpu-baseline "${C[@]}" || exit $?
+               grep '^{' "$D/clock.log" > "$D/bench_clock.json"
+               python tools/timed_launches.py "$D/prof/run_kernel_trace.csv" "$D/kernel_timed_launches.json" > /dev/null &&
+               python tools/sq_summary.py "$D" "$cfg" --out "$OUT/sq_issue.json" > "$D/sq_summary.txt" &&
+               python tools/pmc_summary.py "$D" "$cfg" --out "$OUT/pmc_traffic.json" > "$D/pmc_summary.txt" || exit 4
+             done ;;
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
   esac

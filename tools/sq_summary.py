@@ -28,27 +28,35 @@ def main():
     ap.add_argument("--kernel", default="k_bake")
     ap.add_argument("--out", default=os.path.join(os.path.dirname(__file__), "..", "profiles", "sq_issue.json"))
     a = ap.parse_args()
+    # per (instance, counter): the sum over its dispatches and the dispatch ids. A bake launch of the
+    # launch-tail pair runs two k_bake instances: its per-launch figure is the sum of their per-dispatch means
     tot = collections.defaultdict(float)
     ids = collections.defaultdict(set)
+    first = {}
     src = {}
-    kernel = None
     for step in PASSES:
         for p in glob.glob(os.path.join(a.session, step, "**", "*counter_collection.csv"), recursive=True):
             for r in csv.DictReader(open(p)):
-                if a.kernel not in r["Kernel_Name"]:
+                k = r["Kernel_Name"]
+                if a.kernel not in k:
                     continue
-                kernel = r["Kernel_Name"]
                 c = r["Counter_Name"]
                 if c in src and src[c] != step:
                     continue  # a counter collected in several passes: keep the first pass's value
                 src[c] = step
-                tot[c] += float(r["Counter_Value"])
-                ids[c].add(r.get("Dispatch_Id", r.get("Correlation_Id", "")))
+                tot[k, c] += float(r["Counter_Value"])
+                d = r.get("Dispatch_Id", r.get("Correlation_Id", ""))
+                ids[k, c].add(d)
+                first[k] = min(first.get(k, float("inf")), float(d or 0))
     if not tot:
         raise SystemExit(f"no {a.kernel} dispatch in the counter files of {a.session}")
-    per = {k: tot[k] / max(len(ids[k]), 1) for k in sorted(tot)}
+    names = sorted(first, key=first.get)  # launch order: the saving instance before the resuming one
+    per = collections.defaultdict(float)
+    for (k, c), v in tot.items():
+        per[c] += v / max(len(ids[k, c]), 1)
+    per = dict(sorted(per.items()))
     rec = {
-        "kernel": kernel,
+        "kernel": " + ".join(names),
         "source": f"{a.session}/{{{','.join(PASSES)}}}: rocprofv3 --pmc passes (tools/gpu_session.sh steps sq, sq3, "
                   "grbm, tcp), per dispatch",
         "pass_of": src,

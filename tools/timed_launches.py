@@ -18,7 +18,14 @@ def main():
     rec = {"source": f"{a.trace} (rocprofv3 --kernel-trace of python bench.py; the first {a.warmup} "
                      "dispatch(es) of each kernel are the warm-up steps)"}
     for k in ("k_bake", "k_bucket_fold"):
-        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in rows if k in r["Kernel_Name"]]
+        sel = [r for r in rows if k in r["Kernel_Name"]]
+        ms = [(int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e6 for r in sel]
+        # a bake launch of the launch-tail pair is two dispatches of two instances, back to back: one figure
+        # per launch (bench.py's HIP events bracket the pair)
+        n = len({r["Kernel_Name"] for r in sel}) or 1
+        if n > 1:
+            rec[f"{k}_instances"] = sorted({r["Kernel_Name"] for r in sel}, key=lambda x: [r["Kernel_Name"] for r in sel].index(x))
+            ms = [sum(ms[i:i + n]) for i in range(0, len(ms) - n + 1, n)]
         rec[f"{k}_ms_per_dispatch"] = ms
         timed = ms[a.warmup:]
         rec[f"{k}_timed_mean_ms"] = sum(timed) / len(timed) if timed else None
