@@ -352,8 +352,11 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
    wrap ~1/64 of the time), 2 = R as well (the default: fewer bank dwords per add, -2 % on box200's fold). The sum mod 2^64 is the same either way: a channel is
    hi * 2^32 + lo, and only hi mod 2^32 matters mod 2^64. The carry channels reuse the u64 array's 8 B per texel
    as lo[T] | hi[T]. */
-template <int EXP, int TB = FMGI_TILE_BITS, int SPLIT = 1, int CARRY = 0>
-__global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restrict__ pool,
+/* NB: blocks a wave has in flight, as whole-block register buffers (2: the block being summed and the next;
+   more need the registers of fewer waves: NB > 2 instances are launched where the tile's LDS already holds
+   a CU to one 1024-lane workgroup, i.e. 4 waves per SIMD and 128 VGPRs) */
+template <int EXP, int TB = FMGI_TILE_BITS, int SPLIT = 1, int CARRY = 0, int NB = 2>
+__global__ __launch_bounds__(1024, NB > 2 ? 1 : 8) void k_bucket_fold(const uint32_t *__restrict__ pool,
                                                      const uint32_t *__restrict__ list,
                                                      const uint32_t *__restrict__ block_len,
                                                      const uint32_t *__restrict__ counts, int P, int G,
@@ -425,11 +428,11 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
             lb = list[off + j_lo + wave + (k0 + lane) * waves];
             ll = min(block_len[lb], BP);
         }
-        u32x4 q[4];
-        uint32_t len = 0;
+        u32x4 q[NB][4];
+        uint32_t len[NB];
         /* the whole 4-KB block, unconditionally (codes past the block's length are skipped when summed):
            four 16-B loads per lane with no branch around them, so the wait before a block's sums leaves
-           the next block's loads in flight (loads under a lane condition compiled to 16 dword loads each,
+           the next blocks' loads in flight (loads under a lane condition compiled to 16 dword loads each,
            and the wait at the branch's join waited for the prefetch too) */
         auto fetch = [&](uint32_t k, u32x4 (&qq)[4], uint32_t &ln) {
             const uint32_t b = (uint32_t)__builtin_amdgcn_readlane((int)lb, (int)k);
@@ -439,19 +442,15 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
 #pragma unroll
             for (int u = 0; u < 4; u++) qq[u] = blk[64 * u + lane]; /* codes 4 i4 .. 4 i4 + 3, i4 = 64 u + lane */
         };
-        fetch(0, q, len);
-        for (uint32_t k = 0; k < kn; k++) {
-            u32x4 qn[4];
-            uint32_t lenn = 0;
-            fetch(k + 1 < kn ? k + 1 : k, qn, lenn); /* (the last one re-reads this block: unused) */
+        auto sum = [&](const u32x4 (&qq)[4], uint32_t ln) {
 #pragma unroll
             for (int u = 0; u < 4; u++) {
                 const uint32_t i0 = 4 * (64 * u + lane);
-                const uint32_t cs[4] = {q[u].x, q[u].y, q[u].z, q[u].w};
+                const uint32_t cs[4] = {qq[u].x, qq[u].y, qq[u].z, qq[u].w};
 #pragma unroll
                 for (int m = 0; m < 4; m++) {
                     const uint32_t c = cs[m];
-                    if (i0 + m >= len || c == kSentinel) continue; /* runs are padded to 4 codes */
+                    if (i0 + m >= ln || c == kSentinel) continue; /* runs are padded to 4 codes */
                     if (SPLIT > 1 && (((c >> 10) & kBucketMask) >> TB) != part) continue; /* another fold tile's */
                     const int tx = (int)((c >> 10) & (kTileTexels - 1));
                     if (EXP == 1) {
@@ -464,6 +463,21 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
                     }
                     const uint4 cc = EXP == 4 ? make_uint4(c & 1023, (c & 3) ? c & 511 : 0u, (c & 3) ? c & 255 : 0u, 0u)
                                               : col[c & 1023];
+                    if (CARRY == 3) {
+                        /* R and B - R in one 64-bit word per texel, {B - R : R}: one returning ds_add_rtn_u64 per
+                           code; R's wraps (the hardware carries them into the high half) are counted in cR and
+                           the high half's own wraps in cD, both from the returned old value */
+                        uint32_t *cR = (uint32_t *)acc_g, *cD = cR + kTileTexels;
+                        const uint32_t R = cc.x, D = cc.z;
+                        const unsigned long long old = atomicAdd(&acc_r[tx], ((unsigned long long)D << 32) | R);
+                        const uint32_t lo = (uint32_t)old, cin = (uint32_t)(lo + R < lo);
+                        const unsigned long long hs = (old >> 32) + (unsigned long long)D + cin;
+                        const int dD = (int)(hs >> 32) - (int)((int32_t)D < 0);
+                        if (cin) atomicAdd(&cR[tx], 1u);
+                        if (dD) atomicAdd(&cD[tx], (uint32_t)dD);
+                        if (cc.y) carry_add((uint32_t *)acc_b, kTileTexels, tx, cc.y);
+                        continue;
+                    }
                     if (CARRY >= 2) carry_add((uint32_t *)acc_r, kTileTexels, tx, cc.x);
                     else atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
                     if (EXP == 3) continue;
@@ -476,18 +490,36 @@ __global__ __launch_bounds__(1024, 8) void k_bucket_fold(const uint32_t *__restr
                     if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
                 }
             }
+        };
+        /* a ring of NB blocks: block k is summed from buffer k % NB once block k + NB - 1's loads are issued
+           into the buffer block k - 1 left (the unrolled steps keep every buffer index static) */
 #pragma unroll
-            for (int u = 0; u < 4; u++) q[u] = qn[u];
-            len = lenn;
+        for (int s0 = 0; s0 < NB - 1; s0++) fetch(s0 < (int)kn ? (uint32_t)s0 : kn - 1, q[s0], len[s0]);
+        for (uint32_t kb = 0; kb < kn; kb += NB) {
+#pragma unroll
+            for (int s0 = 0; s0 < NB; s0++) {
+                const uint32_t k = kb + (uint32_t)s0;
+                if (k >= kn) break; /* uniform */
+                const uint32_t kf = k + NB - 1 < kn ? k + NB - 1 : kn - 1; /* (past the end: re-reads, unused) */
+                fetch(kf, q[(s0 + NB - 1) % NB], len[(s0 + NB - 1) % NB]);
+                sum(q[s0], len[s0]);
+            }
         }
     }
     __syncthreads();
     for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
         const int texel = (int)((t << (TB + kSplitBits)) + part * kTileTexels) + i;
         if (texel >= num_texels) break;
-        const unsigned long long r = CARRY >= 2 ? carry_val((const uint32_t *)acc_r, kTileTexels, i) : acc_r[i];
-        const unsigned long long ag = CARRY >= 1 ? carry_val((const uint32_t *)acc_g, kTileTexels, i) : acc_g[i];
-        const unsigned long long ab = CARRY >= 1 ? carry_val((const uint32_t *)acc_b, kTileTexels, i) : acc_b[i];
+        unsigned long long r = CARRY >= 2 ? carry_val((const uint32_t *)acc_r, kTileTexels, i) : acc_r[i];
+        unsigned long long ag = CARRY >= 1 ? carry_val((const uint32_t *)acc_g, kTileTexels, i) : acc_g[i];
+        unsigned long long ab = CARRY >= 1 ? carry_val((const uint32_t *)acc_b, kTileTexels, i) : acc_b[i];
+        if (CARRY == 3) { /* R = cR * 2^32 + the low half; B - R = {cD : high half} - cR; G - R from acc_b */
+            const uint32_t *cR = (const uint32_t *)acc_g, *cD = cR + kTileTexels;
+            const unsigned long long w = acc_r[i];
+            r = ((unsigned long long)cR[i] << 32) | (uint32_t)w;
+            ab = ((((unsigned long long)cD[i] << 32) | (w >> 32)) - cR[i]);
+            ag = carry_val((const uint32_t *)acc_b, kTileTexels, i);
+        }
         const unsigned long long gg = r + ag, bb = r + ab;
         unsigned long long *qq = lm + 4 * (size_t)texel;
         if (r) atomicAdd(qq + 0, r);
@@ -720,6 +752,12 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
             const bool plain = split == 1 && (tb == 12 || exp == 0);
             if (plain && ce && carry == 0) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1> : (FoldFn)k_bucket_fold<0>;
             if (plain && carry == 1) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 1> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1>;
+            if (plain && carry == 3) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 3> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 3>;
+            if (const char *nbe = fmgi_exp_env("FMGI_FOLD_NB")) { /* blocks in flight per wave, wide tiles */
+                const int nbv = atoi(nbe);
+                if (split == 1 && tb == 12 && nbv == 3) fn = k_bucket_fold<0, 12, 1, 2, 3>;
+                if (split == 1 && tb == 12 && nbv == 4) fn = k_bucket_fold<0, 12, 1, 2, 4>;
+            }
         }
 #endif
         if (!fn) return hipErrorInvalidValue; /* no instance for this tile width and split */
