@@ -21,6 +21,7 @@
  */
 #include <hip/hip_runtime.h>
 #include <stdlib.h>
+#include <stdio.h>
 
 #include <algorithm>
 
@@ -695,9 +696,16 @@ int fmgi_fold_split(int tb) {
     const char *e = fmgi_exp_env("FMGI_FOLD_SPLIT");
     const int env = e ? atoi(e) : 0;
     const int want = env > 0 ? env : FMGI_FOLD_SPLIT_DEFAULT;
-    if (tb == 12 && (want == 1 || want == 2)) return want;
-    if (tb == 13) return want == 4 ? 4 : 2; /* 8192-texel fold tiles do not fit LDS */
-    return 1;
+    int got = 1;
+    if (tb == 12 && (want == 1 || want == 2)) got = want;
+    else if (tb == 13) got = want == 4 ? 4 : 2; /* 8192-texel fold tiles do not fit LDS */
+    if (env > 0 && got != env) { /* an A/B would otherwise measure another split than the one it names */
+        static bool said = false;
+        if (!said) fprintf(stderr, "fmgi: FMGI_FOLD_SPLIT=%d has no fold instance for %d-texel buckets: split %d\n",
+                           env, 1 << tb, got);
+        said = true;
+    }
+    return got;
 }
 
 hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long long *lm, hipStream_t s) {

@@ -928,8 +928,11 @@ enum { kStreamSliced = 0, kStreamSegments = 1, kStreamBuckets = 2, kStreamDense 
    the other lanes of its wave finish an item each; plus each wave's last partly written block */
 static uint64_t dense_cap_for(uint64_t items, int grid, int block) {
     const uint64_t waves = (uint64_t)grid * (uint64_t)(block / 64);
-    return items * (FMGI_EVENTS_PER_ITEM + FMGI_PHOTONS_PER_ITEM) +
-           waves * (64ull * (FMGI_EVENTS_PER_ITEM + FMGI_PHOTONS_PER_ITEM) + 2 * FMGI_STREAM_BLOCK);
+    const uint64_t cap = items * (FMGI_EVENTS_PER_ITEM + FMGI_PHOTONS_PER_ITEM) +
+                         waves * (64ull * (FMGI_EVENTS_PER_ITEM + FMGI_PHOTONS_PER_ITEM) + 2 * FMGI_STREAM_BLOCK);
+    /* a whole number of blocks: k_bin reads min(cursor, cap) codes in whole 512-code wave batches, so an
+       overflowed stream still ends on a block boundary inside the buffer */
+    return (cap + FMGI_STREAM_BLOCK - 1) / FMGI_STREAM_BLOCK * FMGI_STREAM_BLOCK;
 }
 
 /* the bucketed stream's pool, in blocks: every code of the chunk, plus one partly filled bucket per wave
