@@ -1812,7 +1812,7 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
     if (kernel < FMGI_KERNEL_EXACT || kernel > FMGI_KERNEL_HYBRID) return set_err(FMGI_ERR_ARG, "bad kernel %d", kernel);
     const bool was_auto = kernel == FMGI_KERNEL_AUTO;
     /* the kernel instance's accumulation: the bucket layout of the stream has its own (kAccBucket) */
-    const int kacc = exec_accum(c);
+    int kacc = exec_accum(c);
     if (was_auto) kernel = c->auto_kernel;
     /* an image too large for LDS: same results, other scan (checked with the LDS of the instance launched) */
     kernel = fitting_kernel(c, kernel, kacc, bake_block());
@@ -1827,7 +1827,17 @@ static int bake_common(fmgi_context *c, uint64_t b, uint64_t e, void *lm, int ke
             (uint64_t)grid_blocks(c, FMGI_KERNEL_FAST, kacc, trace, fp.block, fp.bytes, UINT64_MAX) * fp.block;
         if ((e - b) * 2 <= lanes_max) kernel = FMGI_KERNEL_FAST;
     }
-    const StagePlan sp = plan_stage(c, kernel, kacc, trace);
+    StagePlan sp = plan_stage(c, kernel, kacc, trace);
+    /* the lane-by-lane stores pay only when the loop reads no global table (exec_accum's AUTO choice checks
+       the tables' size, the plan whether they were staged): a plan that left the walls, or a closed box's
+       cells, in global memory takes the rings instead (box2000 before its compact tables: 160 ms scattered,
+       132 ms with the rings) */
+    if (kacc == kAccScatter && c->opt[FMGI_OPT_BUCKET_FILL] < 0 && !c->compact &&
+        ((c->nrects > 0 && sp.rects_off < 0) || (c->cells_lds && kernel == FMGI_KERNEL_GRID && sp.cells_off < 0)) &&
+        fitting_kernel(c, kernel, kAccBucket, bake_block()) == kernel) {
+        kacc = kAccBucket;
+        sp = plan_stage(c, kernel, kacc, trace);
+    }
     const int block = sp.block;
     /* the closed box with every table staged (walls, emitters, grid cells) launches the instance whose
        global-memory paths for them are compiled out (FMGI_KVAR_STAGED); FMGI_NO_STAGED=1 (experiments) keeps
