@@ -15,6 +15,7 @@
   apartment30 (654 walls, 34 sources; the grid's per-axis walk with binary search and records-box
             skip): per-photon traces and a lightmap prefix against the oracle
 """
+import hashlib
 import os
 
 import numpy as np
@@ -152,6 +153,10 @@ def test_config3_full_lightmap_exact(torch_cuda, box200, offsets, capsys):
     assert np.array_equal(part[:, :3], olm)
     for k, key in enumerate(keys):
         assert ost[key] == int(fx["stats"][r, k]), key
+    # the range's own lightmap against the fixture's digest of it (the summed lightmap alone could drift
+    # while the counters hold)
+    digest = hashlib.sha256(np.ascontiguousarray(olm, np.int64).tobytes()).digest()
+    assert digest == fx["range_sha256"][r].tobytes()
 
 
 @pytest.mark.timeout(600)
