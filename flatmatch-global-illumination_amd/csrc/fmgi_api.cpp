@@ -1047,11 +1047,18 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
            7.31 / 6.34 / 5.97 ms at 8 / 4 / 16 / 32 groups per tile, profiles/r03/s33) */
         /* (wide bucket tiles: one 96-KB fold workgroup per CU instead of two, so half the rounds; box200 fold
            11.93 / 11.58 / 11.91 ms at ~408 / 200 / 300 groups per tile, profiles/r05/s26-s27) */
+        /* (wide tiles, round 6: the balanced share gives every workgroup the same blocks, so a round of them
+           ends together and a partly filled last round idles CUs; the groups per tile are rounded DOWN to the
+           launch's multiple of 8 so the workgroups fill just under 13 rounds: box200 (23 tiles, 144 groups,
+           12.94 rounds) 11.50 -> 11.30 ms, box2000 (26 tiles, 128 groups, 13.0 rounds) 11.57 -> 11.24 ms;
+           12.2, 13.7 or 14.4 rounds took 11.45-11.70 ms, profiles/r06/s24-s25) */
         const bool wide = mode >= kStreamBuckets && tbits > FMGI_TILE_BITS && fmgi_fold_split(tbits) == 1;
-        const int rounds = mode >= kStreamBuckets ? (wide ? 18 : 36) : (mode == kStreamSegments ? 16 : 48);
+        const int rounds = mode >= kStreamBuckets ? (wide ? 13 : 36) : (mode == kStreamSegments ? 16 : 48);
         /* (a split bucket tile gets `split` workgroups per group: the same rounds over the fold tiles) */
         const int split = mode >= kStreamBuckets ? fmgi_fold_split(tbits) : 1;
-        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge) : std::max(1, (rounds * ncu + Pf * split - 1) / (Pf * split));
+        sb.groups = (ge && atoi(ge) > 0) ? atoi(ge)
+                    : wide ? std::max(8, (rounds * ncu / (Pf * split)) & ~7)
+                           : std::max(1, (rounds * ncu + Pf * split - 1) / (Pf * split));
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
            or 16 chain blocks (one per wave), per workgroup */
