@@ -1052,13 +1052,18 @@ static int ensure_stream(fmgi_context *c, int k, uint64_t items, int grid, int b
            launch's multiple of 8 so the workgroups fill just under 13 rounds: box200 (23 tiles, 144 groups,
            12.94 rounds) 11.50 -> 11.30 ms, box2000 (26 tiles, 128 groups, 13.0 rounds) 11.57 -> 11.24 ms;
            12.2, 13.7 or 14.4 rounds took 11.45-11.70 ms, profiles/r06/s24-s25) */
+        /* (narrow bucket tiles, round 6: only launches of < 3e6 items use them now, whose streams are small; the
+           per-workgroup set-up and 2048-texel flush then dominate, and 7 whole rounds of the two workgroups per
+           CU beat the 18 the round-3 box200 count gave: example.png fold 1.35 -> 0.85 ms (56 tiles, 64 groups;
+           0.86-0.96 ms at 16-48 groups, 1.06 at 128, 1.55 at 192; profiles/r06/s27-s28) */
         const bool wide = mode >= kStreamBuckets && tbits > FMGI_TILE_BITS && fmgi_fold_split(tbits) == 1;
-        const int rounds = mode >= kStreamBuckets ? (wide ? 13 : 36) : (mode == kStreamSegments ? 16 : 48);
+        const bool buckets = mode >= kStreamBuckets && fmgi_fold_split(tbits) == 1;
+        const int rounds = mode >= kStreamBuckets ? (wide ? 13 : 14) : (mode == kStreamSegments ? 16 : 48);
         /* (a split bucket tile gets `split` workgroups per group: the same rounds over the fold tiles) */
         const int split = mode >= kStreamBuckets ? fmgi_fold_split(tbits) : 1;
         sb.groups = (ge && atoi(ge) > 0) ? atoi(ge)
-                    : wide ? std::max(8, (rounds * ncu / (Pf * split)) & ~7)
-                           : std::max(1, (rounds * ncu + Pf * split - 1) / (Pf * split));
+                    : buckets ? std::max(8, (rounds * ncu / (Pf * split)) & ~7)
+                              : std::max(1, (rounds * ncu + Pf * split - 1) / (Pf * split));
         /* a small stream (config 1: ~8,600 segments at most) would leave most of those workgroups' waves
            without work, and each pays its LDS set-up and tile flush: at least 1024 segments (64 per wave),
            or 16 chain blocks (one per wave), per workgroup */
