@@ -284,6 +284,14 @@ __device__ __forceinline__ void carry_add(uint32_t *lo, int T, int tx, uint32_t 
 __device__ __forceinline__ unsigned long long carry_val(const uint32_t *lo, int T, int i) {
     return ((unsigned long long)lo[T + i] << 32) | lo[i];
 }
+/* k_bucket_fold's split colour table (CARRY >= 4): state i's {R | (G != R) << 31, B - R} as 8 B at slot
+   colour_slot(i), its G - R as 4 B at the same slot of a second array read only by the lanes whose flag is
+   set. The slot XORs the low five bits with the high bits times 3, so the powers of two (a photon's
+   untinted states, the most frequent) take distinct bank pairs (CARRY 5: no swizzle) */
+template <int CARRY>
+__device__ __forceinline__ uint32_t colour_slot(uint32_t i) {
+    return CARRY == 4 ? i ^ (((i >> 5) * 3u) & 31u) : i;
+}
 constexpr int kListPerThread = 8;
 
 __global__ __launch_bounds__(kListThreads) void k_bucket_count(const uint32_t *__restrict__ block_tile,
@@ -352,7 +360,10 @@ __global__ __launch_bounds__(kListThreads) void k_bucket_list(const uint32_t *__
    when old + v >= old): 0 = every channel as one ds_add_u64, 1 = G - R and B - R with carries (their adds
    wrap ~1/64 of the time), 2 = R as well (the default: fewer bank dwords per add, -2 % on box200's fold). The sum mod 2^64 is the same either way: a channel is
    hi * 2^32 + lo, and only hi mod 2^32 matters mod 2^64. The carry channels reuse the u64 array's 8 B per texel
-   as lo[T] | hi[T]. */
+   as lo[T] | hi[T]. 4 and 5 = 2 with the split colour table (colour_slot): the fold's LDS work is counted in
+   dwords, and the 16-B colour read was two thirds of a box200 code's; 5 (the default since profiles/r06/s31)
+   reads 8 B per code plus 4 B for the tinted ones: box200 11.30 -> 9.89 ms, example 0.87 -> 0.74 ms, bit-identical;
+   4's swizzled slots measured 10.07 ms. */
 /* NB: blocks a wave has in flight, as whole-block register buffers (2: the block being summed and the next;
    more need the registers of fewer waves: NB > 2 instances are launched where the tile's LDS already holds
    a CU to one 1024-lane workgroup, i.e. 4 waves per SIMD and 128 VGPRs) */
@@ -411,7 +422,18 @@ __global__ __launch_bounds__(1024, NB > 2 ? 1 : 8) void k_bucket_fold(const uint
     }
     if (j_lo >= j_hi) return; /* uniform */
     for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
-    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
+    uint2 *col2 = (uint2 *)col;                         /* CARRY >= 4: {R | G-flag, B - R} per slot */
+    uint32_t *colg = (uint32_t *)(col2 + FMGI_COLOUR_STATES); /* CARRY >= 4: G - R per slot */
+    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) {
+        const uint4 v = colpack[i];
+        if (CARRY >= 4) {
+            const uint32_t p = colour_slot<CARRY>((uint32_t)i);
+            col2[p] = make_uint2(v.x | (v.y ? 0x80000000u : 0u), v.z); /* R < 2^30 */
+            colg[p] = v.y;
+        } else {
+            col[i] = v;
+        }
+    }
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int waves = blockDim.x >> 6;
@@ -460,6 +482,14 @@ __global__ __launch_bounds__(1024, NB > 2 ? 1 : 8) void k_bucket_fold(const uint
                     }
                     if (EXP == 2) {
                         atomicAdd(&acc_r[tx], 1ull);
+                        continue;
+                    }
+                    if (CARRY >= 4) { /* an 8-B colour read per code, the 4-B G - R only where G != R */
+                        const uint32_t p = colour_slot<CARRY>(c & 1023);
+                        const uint2 rb = col2[p];
+                        carry_add((uint32_t *)acc_r, kTileTexels, tx, rb.x & 0x7FFFFFFFu);
+                        if (rb.y) carry_add((uint32_t *)acc_b, kTileTexels, tx, rb.y);
+                        if ((int32_t)rb.x < 0) carry_add((uint32_t *)acc_g, kTileTexels, tx, colg[p]);
                         continue;
                     }
                     const uint4 cc = EXP == 4 ? make_uint4(c & 1023, (c & 3) ? c & 511 : 0u, (c & 3) ? c & 255 : 0u, 0u)
@@ -741,12 +771,13 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
                            sb.tile_blocks, sb.tile_blocks + FMGI_PRESORT_MAX_TILES + 1, sb.block_list);
         typedef void (*FoldFn)(const uint32_t *, const uint32_t *, const uint32_t *, const uint32_t *, int, int, int,
                                const uint4 *, unsigned long long *, int);
-        /* the channels summed as u32 low words with carry words (CARRY = 2): box200's wide fold 11.76 -> 11.54 ms,
-           bit-identical (profiles/r06/s5 ab_carry.log); the experiment build's FMGI_FOLD_CARRY=0 keeps the
-           int64 adds */
+        /* the channels summed as u32 low words with carry words (CARRY >= 2): box200's wide fold 11.76 -> 11.54 ms,
+           bit-identical (profiles/r06/s5 ab_carry.log); with the split colour table (CARRY = 5: an 8-B colour read
+           per code, G - R only for the tinted states) 11.30 -> 9.89 ms (profiles/r06/s31); the experiment build's
+           FMGI_FOLD_CARRY=0 keeps the int64 adds, =2 the 16-B colour reads */
         FoldFn fn = nullptr;
-        if (split == 1 && tb == FMGI_TILE_BITS) fn = k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
-        else if (split == 1 && tb == 12) fn = k_bucket_fold<0, 12, 1, 2>;
+        if (split == 1 && tb == FMGI_TILE_BITS) fn = k_bucket_fold<0, FMGI_TILE_BITS, 1, 5>;
+        else if (split == 1 && tb == 12) fn = k_bucket_fold<0, 12, 1, 5>;
 #if FMGI_EXPERIMENTS
         {   /* FMGI_EXP_FOLD (profiling variants), FMGI_FOLD_SPLIT (split folds), FMGI_FOLD_CARRY (carry words) */
             const char *xe = fmgi_exp_env("FMGI_EXP_FOLD"), *ce = fmgi_exp_env("FMGI_FOLD_CARRY");
@@ -760,7 +791,10 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
             const bool plain = split == 1 && (tb == 12 || exp == 0);
             if (plain && ce && carry == 0) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1> : (FoldFn)k_bucket_fold<0>;
             if (plain && carry == 1) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 1> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 1>;
+            if (plain && carry == 2) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 2> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
             if (plain && carry == 3) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 3> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 3>;
+            if (plain && carry == 4) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 4> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 4>;
+            if (plain && carry == 5) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 5> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 5>;
             if (const char *nbe = fmgi_exp_env("FMGI_FOLD_NB")) { /* blocks in flight per wave, wide tiles */
                 const int nbv = atoi(nbe);
                 if (split == 1 && tb == 12 && nbv == 3) fn = k_bucket_fold<0, 12, 1, 2, 3>;
