@@ -110,16 +110,55 @@ __global__ __launch_bounds__(NT) void k_slice_sort(const uint32_t *__restrict__ 
     for (int k = threadIdx.x; k < total; k += blockDim.x) sorted[b0 + k] = buf[k];
 }
 
+/* k_bucket_fold's CARRY channels: value v (a u32 two's complement int32) added to lo[tx]; hi[tx] (at lo + T)
+   takes the carry or borrow of the 64-bit sum */
+__device__ __forceinline__ void carry_add(uint32_t *lo, int T, int tx, uint32_t v) {
+    const uint32_t old = atomicAdd(&lo[tx], v); /* ds_add_rtn_u32 */
+    const uint32_t nw = old + v;
+    const int delta = (int)(nw < old) - (int)((int32_t)v < 0);
+    if (delta) atomicAdd(&lo[T + tx], (uint32_t)delta);
+}
+__device__ __forceinline__ unsigned long long carry_val(const uint32_t *lo, int T, int i) {
+    return ((unsigned long long)lo[T + i] << 32) | lo[i];
+}
+/* k_bucket_fold's split colour table (CARRY >= 4): state i's {R | (G != R) << 31, B - R} as 8 B at slot
+   colour_slot(i), its G - R as 4 B at the same slot of a second array read only by the lanes whose flag is
+   set. The slot XORs the low five bits with the high bits times 3, so the powers of two (a photon's
+   untinted states, the most frequent) take distinct bank pairs (CARRY 5: no swizzle) */
+template <int CARRY>
+__device__ __forceinline__ uint32_t colour_slot(uint32_t i) {
+    return CARRY == 4 ? i ^ (((i >> 5) * 3u) & 31u) : i;
+}
+/* the split colour table in LDS (k_bucket_fold's CARRY 5 and the slice-sorted folds): colour state i's
+   {R | (G != R) << 31, B - R} at col2[i], its G - R at colg[i] */
+__device__ __forceinline__ void stage_split_colours(const uint4 *colpack, uint2 *col2, uint32_t *colg) {
+    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) {
+        const uint4 v = colpack[i];
+        col2[i] = make_uint2(v.x | (v.y ? 0x80000000u : 0u), v.z); /* R < 2^30 */
+        colg[i] = v.y;
+    }
+}
+/* one code's exact sums into the carry-word channels of a T-texel tile (acc: R, G - R, B - R, each as
+   lo[T] | hi[T]): an 8-B colour read, the R add, B - R where nonzero, G - R only for the tinted states */
+__device__ __forceinline__ void sum_code_split(unsigned long long *acc, int T, int tx, const uint2 *col2,
+                                               const uint32_t *colg, uint32_t c) {
+    uint32_t *lo = (uint32_t *)acc;
+    const uint2 rb = col2[c & 1023];
+    carry_add(lo, T, tx, rb.x & 0x7FFFFFFFu);
+    if (rb.y) carry_add(lo + 4 * T, T, tx, rb.y);
+    if ((int32_t)rb.x < 0) carry_add(lo + 2 * T, T, tx, colg[c & 1023]);
+}
+
 __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__ sorted,
                                                    const uint16_t *__restrict__ toff,
                                                    const unsigned long long *__restrict__ n_ptr, uint64_t cap,
                                                    int P, int G, const uint4 *__restrict__ colpack,
                                                    unsigned long long *__restrict__ lm, int num_texels) {
-    /* per texel of the tile: sum R, sum (G - R), sum (B - R) (int64 modulo 2^64; the true sums of G and
-       B are non-negative), so a grey code costs one LDS add and a tinted one three */
+    /* per texel of the tile: sum R, sum (G - R), sum (B - R) (modulo 2^64 as carry-word channels; the true
+       sums of G and B are non-negative) with the split colour table (sum_code_split), as k_bucket_fold */
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
-    unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
-    uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
+    uint2 *col2 = (uint2 *)(s_acc + 3 * kTileTexels);
+    uint32_t *colg = (uint32_t *)(col2 + FMGI_COLOUR_STATES);
     /* XCD-aware order: the dispatcher deals workgroups to the 8 XCDs round-robin (workgroup i -> XCD
        i % 8), so XCD x gets groups g = x, x + 8, ... and, within a group, consecutive tiles back to
        back: the runs of neighbouring tiles share the cache lines at their boundaries, and those reads
@@ -131,7 +170,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
     const uint64_t b_lo = ns * g / G, b_hi = ns * (g + 1) / G;
     if (b_lo >= b_hi) return; /* uniform */
     for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
-    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
+    stage_split_colours(colpack, col2, colg);
     __syncthreads();
     const int wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6), lane = threadIdx.x & 63;
     const int waves = blockDim.x >> 6;
@@ -150,10 +189,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
             for (int u = 0; u < 4; u++) {
                 if (v[u] == kSentinel) continue;
                 const int tx = (int)((v[u] >> 10) & (kTileTexels - 1));
-                const uint4 cc = col[v[u] & 1023];
-                atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
-                if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
-                if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
+                sum_code_split(s_acc, kTileTexels, tx, col2, colg, v[u]);
             }
         }
     }
@@ -161,7 +197,10 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
     for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
         const int texel = t * kTileTexels + i;
         if (texel >= num_texels) break;
-        const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
+        const uint32_t *lo = (const uint32_t *)s_acc;
+        const unsigned long long r = carry_val(lo, kTileTexels, i);
+        const unsigned long long gg = r + carry_val(lo + 2 * kTileTexels, kTileTexels, i);
+        const unsigned long long bb = r + carry_val(lo + 4 * kTileTexels, kTileTexels, i);
         unsigned long long *q = lm + 4 * (size_t)texel;
         if (r) atomicAdd(q + 0, r);
         if (gg) atomicAdd(q + 1, gg);
@@ -174,7 +213,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs(const uint32_t *__restrict__
    tile's run of every segment directly. A wave takes kW segments at a time and packs their runs onto its
    lanes (runs average SEG / P codes: kW = 16 for the bake's 1024-code segments, 4 for 32768-code slices,
    whose runs are 4x longer and whose packed index costs kW - 1 compares per code); the sums are
-   k_tile_runs' (int64 R, G - R, B - R in LDS). */
+   k_tile_runs' (R, G - R, B - R as carry-word channels in LDS). */
 template <int SEG, int kW>
 __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restrict__ stream,
                                                        const uint16_t *__restrict__ toff,
@@ -182,8 +221,8 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
                                                        int P, int G, const uint4 *__restrict__ colpack,
                                                        unsigned long long *__restrict__ lm, int num_texels) {
     extern __shared__ __attribute__((aligned(16))) unsigned long long s_acc[]; /* 3 x [2048] + colours */
-    unsigned long long *acc_r = s_acc, *acc_g = s_acc + kTileTexels, *acc_b = s_acc + 2 * kTileTexels;
-    uint4 *col = (uint4 *)(s_acc + 3 * kTileTexels);
+    uint2 *col2 = (uint2 *)(s_acc + 3 * kTileTexels);
+    uint32_t *colg = (uint32_t *)(col2 + FMGI_COLOUR_STATES);
     const int xcd = blockIdx.x & 7, j = blockIdx.x >> 3; /* XCD-aware order, as k_tile_runs */
     const int t = j % P, g = xcd + 8 * (j / P);
     const uint64_t n = *n_ptr < cap ? *n_ptr : cap;
@@ -192,7 +231,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
     const uint64_t s_lo = ns * g / G, s_hi = ns * (g + 1) / G;
     if (s_lo >= s_hi) return; /* uniform */
     for (int i = threadIdx.x; i < 3 * kTileTexels; i += blockDim.x) s_acc[i] = 0;
-    for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) col[i] = colpack[i];
+    stage_split_colours(colpack, col2, colg);
     __syncthreads();
     /* a wave takes kW segments at a time and packs their runs for tile t onto its 64 lanes: lane L < kW
        reads segment L's run bounds, a wave prefix sum gives each run's first packed index, and packed
@@ -247,10 +286,7 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
             for (int u = 0; u < 4; u++) {
                 if (v[u] == kSentinel) continue;
                 const int tx = (int)((v[u] >> 10) & (kTileTexels - 1));
-                const uint4 cc = col[v[u] & 1023];
-                atomicAdd(&acc_r[tx], (unsigned long long)cc.x);
-                if (cc.y) atomicAdd(&acc_g[tx], (unsigned long long)(long long)(int32_t)cc.y);
-                if (cc.z) atomicAdd(&acc_b[tx], (unsigned long long)(long long)(int32_t)cc.z);
+                sum_code_split(s_acc, kTileTexels, tx, col2, colg, v[u]);
             }
         }
     }
@@ -258,7 +294,10 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
     for (int i = threadIdx.x; i < kTileTexels; i += blockDim.x) {
         const int texel = t * kTileTexels + i;
         if (texel >= num_texels) break;
-        const unsigned long long r = acc_r[i], gg = r + acc_g[i], bb = r + acc_b[i];
+        const uint32_t *lo = (const uint32_t *)s_acc;
+        const unsigned long long r = carry_val(lo, kTileTexels, i);
+        const unsigned long long gg = r + carry_val(lo + 2 * kTileTexels, kTileTexels, i);
+        const unsigned long long bb = r + carry_val(lo + 4 * kTileTexels, kTileTexels, i);
         unsigned long long *qq = lm + 4 * (size_t)texel;
         if (r) atomicAdd(qq + 0, r);
         if (gg) atomicAdd(qq + 1, gg);
@@ -273,25 +312,6 @@ __global__ __launch_bounds__(1024) void k_tile_runs_pre(const uint32_t *__restri
    exactly in LDS as k_tile_runs does. */
 constexpr int kListThreads = 1024;
 
-/* k_bucket_fold's CARRY channels: value v (a u32 two's complement int32) added to lo[tx]; hi[tx] (at lo + T)
-   takes the carry or borrow of the 64-bit sum */
-__device__ __forceinline__ void carry_add(uint32_t *lo, int T, int tx, uint32_t v) {
-    const uint32_t old = atomicAdd(&lo[tx], v); /* ds_add_rtn_u32 */
-    const uint32_t nw = old + v;
-    const int delta = (int)(nw < old) - (int)((int32_t)v < 0);
-    if (delta) atomicAdd(&lo[T + tx], (uint32_t)delta);
-}
-__device__ __forceinline__ unsigned long long carry_val(const uint32_t *lo, int T, int i) {
-    return ((unsigned long long)lo[T + i] << 32) | lo[i];
-}
-/* k_bucket_fold's split colour table (CARRY >= 4): state i's {R | (G != R) << 31, B - R} as 8 B at slot
-   colour_slot(i), its G - R as 4 B at the same slot of a second array read only by the lanes whose flag is
-   set. The slot XORs the low five bits with the high bits times 3, so the powers of two (a photon's
-   untinted states, the most frequent) take distinct bank pairs (CARRY 5: no swizzle) */
-template <int CARRY>
-__device__ __forceinline__ uint32_t colour_slot(uint32_t i) {
-    return CARRY == 4 ? i ^ (((i >> 5) * 3u) & 31u) : i;
-}
 constexpr int kListPerThread = 8;
 
 __global__ __launch_bounds__(kListThreads) void k_bucket_count(const uint32_t *__restrict__ block_tile,
