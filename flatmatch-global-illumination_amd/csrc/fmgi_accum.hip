@@ -446,7 +446,9 @@ __global__ __launch_bounds__(1024, NB > 2 ? 1 : 8) void k_bucket_fold(const uint
     uint32_t *colg = (uint32_t *)(col2 + FMGI_COLOUR_STATES); /* CARRY >= 4: G - R per slot */
     for (int i = threadIdx.x; i < FMGI_COLOUR_STATES; i += blockDim.x) {
         const uint4 v = colpack[i];
-        if (CARRY >= 4) {
+        if (CARRY == 6) {
+            col2[i] = make_uint2(v.y, v.z); /* {G - R, B - R}: read by the tinted codes only */
+        } else if (CARRY >= 4) {
             const uint32_t p = colour_slot<CARRY>((uint32_t)i);
             col2[p] = make_uint2(v.x | (v.y ? 0x80000000u : 0u), v.z); /* R < 2^30 */
             colg[p] = v.y;
@@ -502,6 +504,32 @@ __global__ __launch_bounds__(1024, NB > 2 ? 1 : 8) void k_bucket_fold(const uint
                     }
                     if (EXP == 2) {
                         atomicAdd(&acc_r[tx], 1ull);
+                        continue;
+                    }
+                    if (CARRY == 6) {
+                        /* R from the state's bounce count (a tint scales G and B only): the float replay of
+                           colour_table()'s x channel; an untinted state's B - R the same way; an 8-B {G - R,
+                           B - R} read only for the tinted states */
+                        const uint32_t st = c & 511;
+                        if (st == 0) continue; /* colour 0 */
+                        const int nbn = 31 - __clz((int)st);
+                        float x = (c & 512) ? 18.0f : 16.0f, z = 18.0f;
+#pragma unroll
+                        for (int k = 0; k < 8; k++) {
+                            const bool m = k < nbn;
+                            x = m ? x * 0.9f : x;
+                            z = m ? z * 0.9f : z;
+                        }
+                        const uint32_t R = (uint32_t)(x * 33554432.0f); /* 2^FMGI_FX_SHIFT */
+                        carry_add((uint32_t *)acc_r, kTileTexels, tx, R);
+                        if (st == (1u << nbn)) {
+                            const uint32_t d = (uint32_t)(z * 33554432.0f) - R;
+                            if (d) carry_add((uint32_t *)acc_b, kTileTexels, tx, d);
+                        } else {
+                            const uint2 gb = col2[c & 1023];
+                            if (gb.y) carry_add((uint32_t *)acc_b, kTileTexels, tx, gb.y);
+                            if (gb.x) carry_add((uint32_t *)acc_g, kTileTexels, tx, gb.x);
+                        }
                         continue;
                     }
                     if (CARRY >= 4) { /* an 8-B colour read per code, the 4-B G - R only where G != R */
@@ -814,6 +842,7 @@ hipError_t fmgi_stream_fold(const StreamBufs &sb, int num_texels, unsigned long 
             if (plain && carry == 2) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 2> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 2>;
             if (plain && carry == 3) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 3> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 3>;
             if (plain && carry == 4) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 4> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 4>;
+            if (plain && carry == 6) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 6> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 6>;
             if (plain && carry == 5) fn = tb == 12 ? (FoldFn)k_bucket_fold<0, 12, 1, 5> : (FoldFn)k_bucket_fold<0, FMGI_TILE_BITS, 1, 5>;
             if (const char *nbe = fmgi_exp_env("FMGI_FOLD_NB")) { /* blocks in flight per wave, wide tiles */
                 const int nbv = atoi(nbe);

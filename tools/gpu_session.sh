@@ -28,6 +28,8 @@
 #                    line (bench_<config>.log in $OUT), kernel trace, FETCH/WRITE, SQ, GRBM, TA/TD/TCP passes and the
 #                    clock build; then tools/{timed_launches,sq_summary,pmc_summary}.py over them (the summaries are
 #                    written to $OUT/sq_issue.json and $OUT/pmc_traffic.json; copy them to profiles/ after review)
+#   adopt            copies this session's $OUT/sq_issue.json and pmc_traffic.json over profiles/ on the box, so that
+#                    bench lines later in the session report them (commit the same files after review)
 # Each GPU step has its own time limit; a crash/timeout (rc > 1) stops the session.
 set -u
 cd "$(dirname "$0")/.."
@@ -98,6 +100,7 @@ for s in ${FMGI_STEPS:-tests ref bench prof}; do
                python tools/sq_summary.py "$D" "$cfg" --out "$OUT/sq_issue.json" > "$D/sq_summary.txt" &&
                python tools/pmc_summary.py "$D" "$cfg" --out "$OUT/pmc_traffic.json" > "$D/pmc_summary.txt" || exit 4
              done ;;
+    adopt) cp "$OUT/sq_issue.json" "$OUT/pmc_traffic.json" profiles/ || exit 4 ;; # this session's summaries, for the bench lines after it
     pmc)   step pmc_fetch 600 rocprofv3 --pmc FETCH_SIZE -d "$OUT/pmc_fetch" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} &&
            step pmc_write 600 rocprofv3 --pmc WRITE_SIZE -d "$OUT/pmc_write" -o run --output-format csv -- python bench.py --steps 2 --warmup 1 --no-cpu-baseline ${PROF_ARGS:-} ;;
   esac
